@@ -1,0 +1,624 @@
+// dsr_api.hip — C ABI of libdsr (include/dsr.h): contexts, decoder packing, resident
+// batches and the per-iteration launch sequence of the device Gauss-Newton loop.
+//
+// Build (gfx950 only, in-tree):  make -C dsp-slam-rgbd_amd/csrc   -> libdsr.so
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/dsr.h"
+#include "dsr_kernels.hpp"
+
+using namespace dsr;
+
+struct dsr_ctx {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  std::string err;
+};
+
+struct dsr_decoder {
+  dsr_ctx* ctx = nullptr;
+  float* dmem = nullptr;
+  size_t bytes = 0;
+  DevDecoder D{};
+  int code_len = 64;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct dsr_batch {
+  dsr_ctx* ctx = nullptr;
+  const dsr_decoder* dec = nullptr;
+  GNParams P{};
+  int n_obj = 0;
+  int iters = 0;
+  int M = 50;
+  std::vector<ObjDesc> hdesc;
+  int cand_total = 0, slot_total = 0, fwd_tile_cap = 0, jac_tile_cap = 0;
+  std::vector<void*> allocs;
+  // device
+  ObjDesc* desc = nullptr;
+  ObjState* st = nullptr;
+  float *zbuf = nullptr, *z_in = nullptr, *t_in = nullptr;
+  int* is_oc = nullptr;
+  float *pts = nullptr, *rays = nullptr, *dobs = nullptr;
+  float4 *cand = nullptr, *kpts = nullptr;
+  float *dense = nullptr, *kres = nullptr;
+  float *bias0f = nullptr, *bias4f = nullptr;
+  Tile *tiles_f = nullptr, *tiles_j = nullptr;
+  int *nt_f = nullptr, *nt_j = nullptr;
+  float* slots = nullptr;
+  int* counts = nullptr;
+  dsr_object_out* out = nullptr;
+  float *tr_H = nullptr, *tr_v = nullptr;
+  int* tr_i = nullptr;
+  std::vector<hipEvent_t> ev;   // [iters][4] fwd0 fwd1 jac0 jac1 + begin/end
+  bool ran = false;
+};
+
+#define DSR_CHECK(ctx, call)                                                        \
+  do {                                                                              \
+    hipError_t e_ = (call);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      if (ctx) (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);      \
+      return -1;                                                                    \
+    }                                                                               \
+  } while (0)
+
+static int fail(dsr_ctx* ctx, const std::string& m) {
+  if (ctx) ctx->err = m;
+  return -2;
+}
+
+extern "C" {
+
+int dsr_abi_version(void) { return DSR_ABI_VERSION; }
+
+int dsr_device_count(int* n) {
+  if (!n) return -2;
+  return hipGetDeviceCount(n) == hipSuccess ? 0 : -1;
+}
+
+int dsr_ctx_create(int device, dsr_ctx** out) {
+  if (!out) return -2;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -3;
+  if (device < 0 || device >= n) return -2;
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return -4;
+  auto* c = new dsr_ctx();
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return -1;
+  }
+  *out = c;
+  return 0;
+}
+
+int dsr_ctx_destroy(dsr_ctx* ctx) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return 0;
+}
+
+const char* dsr_last_error(const dsr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+// ------------------------------------------------------------------------------------
+// decoder packing
+// ------------------------------------------------------------------------------------
+// A-fragment layout of v_mfma_f32_16x16x4_f32 with the permuted-k float4 scheme of
+// dsr_mlp.hpp: out[((rb*T + t)*64 + lane)*4 + j] = src(16 rb + (lane&15), 16 t + 4 (lane>>4) + j)
+static void pack_frag(std::vector<float>& out, int rows_pad, int cols_pad,
+                      const std::function<float(int, int)>& src) {
+  const int RB = rows_pad / 16, T = cols_pad / 16;
+  out.assign((size_t)RB * T * 256, 0.f);
+  for (int rb = 0; rb < RB; ++rb)
+    for (int t = 0; t < T; ++t)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 4; ++j)
+          out[(((size_t)rb * T + t) * 64 + lane) * 4 + j] =
+              src(16 * rb + (lane & 15), 16 * t + 4 * (lane >> 4) + j);
+}
+
+int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, size_t n_floats,
+                     dsr_decoder** out) {
+  if (!ctx || !d || !w || !out) return fail(ctx, "null argument");
+  *out = nullptr;
+  // The topology DSP-SLAM ships (deep_sdf_decoder.py with dims=[512]*8, latent_in=[4],
+  // weight_norm, no xyz_in_all, no use_tanh).  Anything else is rejected loudly.
+  static const int od[9] = {512, 512, 512, 445, 512, 512, 512, 512, 1};
+  static const int id[9] = {67, 512, 512, 512, 512, 512, 512, 512, 512};
+  if (d->code_len != CODE) return fail(ctx, "libdsr supports code_len == 64 only");
+  if (d->n_layers != 9) return fail(ctx, "libdsr supports the 9-layer (dims=[512]*8) DeepSDF decoder only");
+  for (int i = 0; i < 9; ++i)
+    if (d->out_dim[i] != od[i] || d->in_dim[i] != id[i])
+      return fail(ctx, "unsupported decoder layer shapes (expected DeepSDF 8x512 with latent_in=[4])");
+  if (d->latent_in != 4) return fail(ctx, "latent_in must be [4]");
+  if (d->use_tanh || d->xyz_in_all) return fail(ctx, "use_tanh / xyz_in_all decoders are not supported");
+  size_t need = 0;
+  std::vector<const float*> W(9), B(9);
+  for (int i = 0; i < 9; ++i) {
+    W[i] = w + need;
+    need += (size_t)od[i] * id[i];
+    B[i] = w + need;
+    need += od[i];
+  }
+  if (n_floats != need) return fail(ctx, "weight buffer has the wrong size");
+  hipSetDevice(ctx->device);
+
+  auto Wat = [&](int l, int r, int c) { return W[l][(size_t)r * id[l] + c]; };
+  std::vector<std::vector<float>> blobs;
+  std::vector<size_t> offs;
+  size_t total = 0;
+  auto add = [&](std::vector<float>&& v) {
+    offs.push_back(total);
+    total += (v.size() + 63) / 64 * 64;     // 256-B alignment
+    blobs.push_back(std::move(v));
+    return (int)blobs.size() - 1;
+  };
+  int hf[8] = {-1}, hb[8] = {-1}, hbias[8] = {-1};
+  int Kf[8] = {0}, Kb[8] = {0};
+  for (int l = 1; l <= 7; ++l) {
+    std::vector<float> v;
+    if (l == 3) {
+      Kf[l] = 512;
+      pack_frag(v, 512, 512, [&](int r, int c) { return r < L3_OUT ? Wat(3, r, c) : 0.f; });
+    } else if (l == 4) {
+      Kf[l] = 448;
+      pack_frag(v, 512, 448, [&](int r, int c) {
+        return c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
+      });
+    } else {
+      Kf[l] = 512;
+      pack_frag(v, 512, 512, [&](int r, int c) { return Wat(l, r, c); });
+    }
+    hf[l] = add(std::move(v));
+  }
+  for (int l = 1; l <= 7; ++l) {
+    std::vector<float> v;
+    if (l == 3) {
+      Kb[l] = 448;
+      pack_frag(v, 512, 448, [&](int r, int c) { return c < L3_OUT ? Wat(3, c, r) : 0.f; });
+    } else {
+      Kb[l] = 512;
+      pack_frag(v, 512, 512, [&](int r, int c) { return Wat(l, c, r); });
+    }
+    hb[l] = add(std::move(v));
+  }
+  {
+    std::vector<float> v;
+    Kb[0] = 512;
+    pack_frag(v, 80, 512, [&](int r, int c) { return r < IN ? Wat(0, c, r) : 0.f; });
+    hb[0] = add(std::move(v));
+  }
+  for (int l = 0; l <= 7; ++l) {
+    std::vector<float> v(512, 0.f);
+    for (int i = 0; i < od[l]; ++i) v[i] = B[l][i];
+    hbias[l] = add(std::move(v));
+  }
+  std::vector<float> w0x(512 * 3), w0z(512 * 64), w4z(512 * 64), w8(512);
+  for (int n = 0; n < 512; ++n) {
+    for (int i = 0; i < 3; ++i) w0x[n * 3 + i] = Wat(0, n, CODE + i);
+    for (int k = 0; k < 64; ++k) {
+      w0z[n * 64 + k] = Wat(0, n, k);
+      w4z[n * 64 + k] = Wat(4, n, L3_OUT + k);
+    }
+    w8[n] = Wat(8, 0, n);
+  }
+  const int h0x = add(std::move(w0x)), h0z = add(std::move(w0z)), h4z = add(std::move(w4z)),
+            h8 = add(std::move(w8));
+
+  auto* dec = new dsr_decoder();
+  dec->ctx = ctx;
+  dec->bytes = total * sizeof(float);
+  if (hipMalloc(&dec->dmem, dec->bytes) != hipSuccess) {
+    delete dec;
+    return fail(ctx, "hipMalloc failed for decoder weights");
+  }
+  std::vector<float> host(total, 0.f);
+  for (size_t i = 0; i < blobs.size(); ++i)
+    std::copy(blobs[i].begin(), blobs[i].end(), host.begin() + offs[i]);
+  if (hipMemcpy(dec->dmem, host.data(), dec->bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(dec->dmem);
+    delete dec;
+    return fail(ctx, "hipMemcpy failed for decoder weights");
+  }
+  auto P = [&](int h) { return dec->dmem + offs[h]; };
+  DevDecoder& D = dec->D;
+  for (int l = 0; l < 8; ++l) {
+    D.Wf[l] = (l >= 1) ? reinterpret_cast<const float4*>(P(hf[l])) : nullptr;
+    D.Kf[l] = Kf[l];
+    D.Wb[l] = reinterpret_cast<const float4*>(P(hb[l]));
+    D.Kb[l] = Kb[l];
+    D.bias[l] = P(hbias[l]);
+  }
+  D.W0x = P(h0x);
+  D.W0z = P(h0z);
+  D.W4z = P(h4z);
+  D.W8 = P(h8);
+  D.b8 = B[8][0];
+  *out = dec;
+  return 0;
+}
+
+int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
+  if (!dec) return 0;
+  hipSetDevice(dec->ctx->device);
+  hipFree(dec->dmem);
+  delete dec;
+  (void)ctx;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// batches
+// ------------------------------------------------------------------------------------
+static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 256;
+  if (hipMalloc(p, bytes) != hipSuccess) return fail(b->ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
+  b->allocs.push_back(*p);
+  return 0;
+}
+
+static GNParams make_params(const dsr_optim_params* p) {
+  GNParams P;
+  P.k1 = p->k1; P.k2 = p->k2; P.k3 = p->k3; P.k4 = p->k4;
+  P.b1 = p->b1; P.b2 = p->b2; P.lr = p->lr; P.s_damp = p->s_damp;
+  P.cut_off = p->cut_off; P.iters = p->num_iterations; P.M = p->num_depth_samples;
+  return P;
+}
+
+int dsr_batch_destroy(dsr_batch* b) {
+  if (!b) return 0;
+  hipSetDevice(b->ctx->device);
+  for (auto& e : b->ev) hipEventDestroy(e);
+  for (void* p : b->allocs) hipFree(p);
+  delete b;
+  return 0;
+}
+
+static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
+                             int n_obj, const dsr_object_in* in, bool trace, dsr_batch** out) {
+  if (!ctx || !dec || !p || !out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
+  *out = nullptr;
+  if (n_obj <= 0) return fail(ctx, "n_obj must be > 0");
+  if (p->code_len != dec->code_len) return fail(ctx, "optimizer code_len != decoder code_len");
+  if (p->num_depth_samples < 2 || p->num_depth_samples > MAXM)
+    return fail(ctx, "num_depth_samples must be in [2, 64]");
+  if (p->num_iterations < 0) return fail(ctx, "num_iterations < 0");
+  hipSetDevice(ctx->device);
+  auto* b = new dsr_batch();
+  b->ctx = ctx;
+  b->dec = dec;
+  b->P = make_params(p);
+  b->n_obj = n_obj;
+  b->iters = p->num_iterations;
+  b->M = p->num_depth_samples;
+  const int M = b->M;
+  std::vector<float> hpts, hrays, hdobs, hz((size_t)n_obj * CODE, 0.f), ht((size_t)n_obj * 16);
+  std::vector<int> hoc(n_obj);
+  int pts_off = 0, ray_off = 0, cand_off = 0, slot_off = 0, ftiles = 0;
+  for (int o = 0; o < n_obj; ++o) {
+    const dsr_object_in& x = in[o];
+    if (x.n_pts <= 0 || !x.pts) { dsr_batch_destroy(b); return fail(ctx, "object has no surface points"); }
+    if (x.n_rays <= 0 || !x.rays) { dsr_batch_destroy(b); return fail(ctx, "object has no rays"); }
+    if (x.n_depth < 0 || x.n_depth > x.n_rays || (x.n_depth > 0 && !x.depth)) {
+      dsr_batch_destroy(b);
+      return fail(ctx, "depth must hold at most n_rays foreground values");
+    }
+    ObjDesc d{};
+    d.pts_off = pts_off; d.n_pts = x.n_pts;
+    d.ray_off = ray_off; d.n_rays = x.n_rays; d.n_fg = x.n_depth;
+    d.cand_off = cand_off; d.slot_sdf = slot_off;
+    b->hdesc.push_back(d);
+    hpts.insert(hpts.end(), x.pts, x.pts + (size_t)x.n_pts * 3);
+    hrays.insert(hrays.end(), x.rays, x.rays + (size_t)x.n_rays * 3);
+    for (int r = 0; r < x.n_rays; ++r) hdobs.push_back(r < x.n_depth ? x.depth[r] : 0.f);
+    if (x.code) std::copy(x.code, x.code + CODE, hz.begin() + (size_t)o * CODE);
+    std::copy(x.t_cam_obj, x.t_cam_obj + 16, ht.begin() + (size_t)o * 16);
+    hoc[o] = x.pose_is_obj_cam ? 1 : 0;
+    const int cap = x.n_rays * M;
+    pts_off += x.n_pts;
+    ray_off += x.n_rays;
+    cand_off += cap;
+    ftiles += (cap + TILE - 1) / TILE;
+    slot_off += (x.n_pts + TILE - 1) / TILE + (cap + TILE - 1) / TILE;
+  }
+  b->cand_total = cand_off;
+  b->slot_total = slot_off;
+  b->fwd_tile_cap = ftiles;
+  b->jac_tile_cap = slot_off;
+  int rc = 0;
+#define ALLOC(ptr, bytes) \
+  if ((rc = batch_alloc(b, (void**)&(ptr), (bytes))) != 0) { dsr_batch_destroy(b); return rc; }
+  ALLOC(b->desc, sizeof(ObjDesc) * n_obj);
+  ALLOC(b->st, sizeof(ObjState) * n_obj);
+  ALLOC(b->zbuf, sizeof(float) * CODE * n_obj);
+  ALLOC(b->z_in, sizeof(float) * CODE * n_obj);
+  ALLOC(b->t_in, sizeof(float) * 16 * n_obj);
+  ALLOC(b->is_oc, sizeof(int) * n_obj);
+  ALLOC(b->pts, sizeof(float) * hpts.size());
+  ALLOC(b->rays, sizeof(float) * hrays.size());
+  ALLOC(b->dobs, sizeof(float) * hdobs.size());
+  ALLOC(b->cand, sizeof(float4) * (size_t)cand_off);
+  ALLOC(b->kpts, sizeof(float4) * (size_t)cand_off);
+  ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
+  ALLOC(b->kres, sizeof(float) * (size_t)cand_off);
+  ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
+  ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
+  ALLOC(b->tiles_f, sizeof(Tile) * (size_t)ftiles);
+  ALLOC(b->tiles_j, sizeof(Tile) * (size_t)slot_off);
+  ALLOC(b->nt_f, sizeof(int));
+  ALLOC(b->nt_j, sizeof(int));
+  ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
+  ALLOC(b->counts, sizeof(int) * 2 * (size_t)std::max(1, b->iters) * n_obj);
+  ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
+  if (trace) {
+    const size_t it = std::max(1, b->iters);
+    ALLOC(b->tr_H, sizeof(float) * NPAR * NPAR * it * n_obj);
+    ALLOC(b->tr_v, sizeof(float) * TRACE_V * it * n_obj);
+    ALLOC(b->tr_i, sizeof(int) * 2 * it * n_obj);
+  }
+#undef ALLOC
+  auto up = [&](void* dst, const void* src, size_t bytes) {
+    return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(b->desc, b->hdesc.data(), sizeof(ObjDesc) * n_obj) ||
+      !up(b->z_in, hz.data(), sizeof(float) * hz.size()) ||
+      !up(b->t_in, ht.data(), sizeof(float) * ht.size()) ||
+      !up(b->is_oc, hoc.data(), sizeof(int) * n_obj) ||
+      !up(b->pts, hpts.data(), sizeof(float) * hpts.size()) ||
+      !up(b->rays, hrays.data(), sizeof(float) * hrays.size()) ||
+      !up(b->dobs, hdobs.data(), sizeof(float) * hdobs.size())) {
+    dsr_batch_destroy(b);
+    return fail(ctx, "hipMemcpy (inputs) failed");
+  }
+  if (trace) {
+    hipMemset(b->tr_H, 0, sizeof(float) * NPAR * NPAR * std::max(1, b->iters) * n_obj);
+    hipMemset(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj);
+    hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
+  }
+  b->ev.resize((size_t)std::max(1, b->iters) * 4 + 2);
+  for (auto& e : b->ev)
+    if (hipEventCreate(&e) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
+  *out = b;
+  return 0;
+}
+
+int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int n_obj,
+                     const dsr_object_in* in, dsr_batch** out) {
+  return batch_create_impl(ctx, dec, p, n_obj, in, false, out);
+}
+
+int dsr_batch_run(dsr_batch* b) {
+  if (!b) return -2;
+  dsr_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  const int n = b->n_obj;
+  const DevDecoder& D = b->dec->D;
+  const GNParams P = b->P;
+  const int grid = ctx->n_cu;
+  const int cb = (n + 63) / 64;
+  DSR_CHECK(ctx, hipEventRecord(b->ev[0], s));
+  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
+  for (int it = 0; it < b->iters; ++it) {
+    hipLaunchKernelGGL(k_iter_begin, dim3(n), dim3(512), 0, s, n, b->desc, b->st, b->zbuf, D, P,
+                       b->bias0f, b->bias4f, b->dobs);
+    hipLaunchKernelGGL(k_sample, dim3(n), dim3(SAMPLE_THREADS), 0, s, n, b->desc, b->st, b->rays, b->M,
+                       b->cand, b->dense);
+    hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_f, b->nt_f);
+    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 0], s));
+    hipLaunchKernelGGL(k_mlp_fwd, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
+                       b->bias0f, b->bias4f, b->dense);
+    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 1], s));
+    hipLaunchKernelGGL(k_render, dim3(n), dim3(RENDER_THREADS), 0, s, n, b->desc, b->st, b->rays, b->dobs, P,
+                       b->dense, b->kpts, b->kres);
+    hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_j, b->nt_j);
+    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 2], s));
+    hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
+                       b->pts, b->kpts, b->kres, b->bias0f, b->bias4f, P, b->slots,
+                       (const float4*)nullptr, (float*)nullptr);
+    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 3], s));
+    hipLaunchKernelGGL(k_count, dim3(cb), dim3(64), 0, s, n, b->desc, b->st, it, b->counts);
+    hipLaunchKernelGGL(k_solve, dim3(n), dim3(SOLVE_THREADS), 0, s, n, b->desc, b->st, b->zbuf, P, b->slots,
+                       b->tr_H, b->tr_v, b->tr_i);
+  }
+  hipLaunchKernelGGL(k_finalize, dim3(cb), dim3(64), 0, s, n, b->st, b->zbuf, b->out);
+  DSR_CHECK(ctx, hipGetLastError());
+  DSR_CHECK(ctx, hipEventRecord(b->ev[1], s));
+  b->ran = true;
+  return 0;
+}
+
+int dsr_batch_sync(dsr_batch* b) {
+  if (!b) return -2;
+  hipSetDevice(b->ctx->device);
+  DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
+  return 0;
+}
+
+int dsr_batch_download(dsr_batch* b, dsr_object_out* out) {
+  if (!b || !out) return -2;
+  hipSetDevice(b->ctx->device);
+  DSR_CHECK(b->ctx, hipMemcpyAsync(out, b->out, sizeof(dsr_object_out) * b->n_obj, hipMemcpyDeviceToHost,
+                                   b->ctx->stream));
+  DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
+  return 0;
+}
+
+int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
+  if (!b || !st) return -2;
+  if (!b->ran) return fail(b->ctx, "batch has not run");
+  hipSetDevice(b->ctx->device);
+  DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
+  std::memset(st, 0, sizeof(*st));
+  float ms = 0.f;
+  for (int it = 0; it < b->iters; ++it) {
+    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[2 + it * 4 + 0], b->ev[2 + it * 4 + 1]));
+    st->fwd_ms += ms;
+    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[2 + it * 4 + 2], b->ev[2 + it * 4 + 3]));
+    st->jac_ms += ms;
+  }
+  DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
+  st->total_ms = ms;
+  st->fwd_launches = st->jac_launches = b->iters;
+  std::vector<int> c((size_t)2 * std::max(1, b->iters) * b->n_obj);
+  DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
+  for (int it = 0; it < b->iters; ++it)
+    for (int o = 0; o < b->n_obj; ++o) {
+      st->fwd_points += c[((size_t)it * b->n_obj + o) * 2 + 0];
+      st->jac_points += c[((size_t)it * b->n_obj + o) * 2 + 1];
+    }
+  return 0;
+}
+
+int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int n_obj,
+                          const dsr_object_in* in, dsr_object_out* out, const dsr_trace* trace) {
+  if (!out) return fail(ctx, "null output");
+  dsr_batch* b = nullptr;
+  int rc = batch_create_impl(ctx, dec, p, n_obj, in, trace != nullptr, &b);
+  if (rc) return rc;
+  rc = dsr_batch_run(b);
+  if (!rc) rc = dsr_batch_download(b, out);
+  if (!rc && trace) {
+    const int it = b->iters;
+    std::vector<float> H((size_t)NPAR * NPAR * std::max(1, it) * n_obj), V((size_t)TRACE_V * std::max(1, it) * n_obj);
+    std::vector<int> I((size_t)2 * std::max(1, it) * n_obj);
+    if (hipMemcpy(H.data(), b->tr_H, sizeof(float) * H.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(V.data(), b->tr_v, sizeof(float) * V.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(I.data(), b->tr_i, sizeof(int) * I.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = fail(ctx, "trace download failed");
+    } else {
+      for (int o = 0; o < n_obj; ++o) {
+        const dsr_trace& t = trace[o];
+        for (int e = 0; e < it; ++e) {
+          const size_t k = (size_t)e * n_obj + o;
+          if (t.H) std::memcpy(t.H + (size_t)e * NPAR * NPAR, H.data() + k * NPAR * NPAR, sizeof(float) * NPAR * NPAR);
+          const float* v = V.data() + k * TRACE_V;
+          if (t.b) std::memcpy(t.b + (size_t)e * NPAR, v, sizeof(float) * NPAR);
+          if (t.dx) std::memcpy(t.dx + (size_t)e * NPAR, v + NPAR, sizeof(float) * NPAR);
+          if (t.loss) t.loss[e] = v[2 * NPAR];
+          if (t.sdf_loss) t.sdf_loss[e] = v[2 * NPAR + 1];
+          if (t.render_loss) t.render_loss[e] = v[2 * NPAR + 2];
+          if (t.t_obj_cam) std::memcpy(t.t_obj_cam + (size_t)e * 16, v + 2 * NPAR + 3, sizeof(float) * 16);
+          if (t.z) std::memcpy(t.z + (size_t)e * CODE, v + 2 * NPAR + 19, sizeof(float) * CODE);
+          if (t.n_valid) t.n_valid[e] = I[k * 2];
+          if (t.k) t.k[e] = I[k * 2 + 1];
+        }
+      }
+    }
+  }
+  dsr_batch_destroy(b);
+  return rc;
+}
+
+// ------------------------------------------------------------------------------------
+// raw decoder queries (dsr_sdf_eval)
+// ------------------------------------------------------------------------------------
+__global__ void k_fold_code(DevDecoder D, const float* __restrict__ z, float* __restrict__ bias0f,
+                            float* __restrict__ bias4f) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= HID) return;
+  float s0 = 0.f, s4 = 0.f;
+  for (int k = 0; k < CODE; ++k) {
+    s0 = __builtin_fmaf(D.W0z[n * CODE + k], z[k], s0);
+    s4 = __builtin_fmaf(D.W4z[n * CODE + k], z[k], s4);
+  }
+  bias0f[n] = D.bias[0][n] + s0;
+  bias4f[n] = D.bias[4][n] + s4;
+}
+
+int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts, int n,
+                 float* sdf, float* jac) {
+  if (!ctx || !dec || !code || (n > 0 && (!pts || !sdf))) return fail(ctx, "null argument");
+  if (n <= 0) return 0;
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  const int nt = (n + TILE - 1) / TILE;
+  std::vector<float4> hp((size_t)nt * TILE, make_float4(0.f, 0.f, 0.f, 0.f));
+  for (int i = 0; i < n; ++i) {
+    float fi;
+    std::memcpy(&fi, &i, sizeof(float));
+    hp[i] = make_float4(pts[i * 3], pts[i * 3 + 1], pts[i * 3 + 2], fi);
+  }
+  std::vector<Tile> ht(nt);
+  for (int t = 0; t < nt; ++t) ht[t] = Tile{0, jac ? 2 : 0, t * TILE, std::min(TILE, n - t * TILE)};
+  ObjDesc d{};
+  d.n_pts = n;
+  void *dp = nullptr, *dz = nullptr, *db0 = nullptr, *db4 = nullptr, *dt = nullptr, *dnt = nullptr,
+       *dout = nullptr, *dd = nullptr;
+  std::vector<void*> al;
+  auto A = [&](void** p, size_t bytes) {
+    if (hipMalloc(p, bytes) != hipSuccess) return false;
+    al.push_back(*p);
+    return true;
+  };
+  auto cleanup = [&]() { for (void* p : al) hipFree(p); };
+  const size_t outw = jac ? (size_t)(IN + 1) : 1;
+  if (!A(&dp, sizeof(float4) * hp.size()) || !A(&dz, sizeof(float) * CODE) || !A(&db0, sizeof(float) * HID) ||
+      !A(&db4, sizeof(float) * HID) || !A(&dt, sizeof(Tile) * nt) || !A(&dnt, sizeof(int)) ||
+      !A(&dout, sizeof(float) * outw * nt * TILE) || !A(&dd, sizeof(ObjDesc))) {
+    cleanup();
+    return fail(ctx, "hipMalloc failed (sdf_eval)");
+  }
+  bool ok = hipMemcpy(dp, hp.data(), sizeof(float4) * hp.size(), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dz, code, sizeof(float) * CODE, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dt, ht.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dnt, &nt, sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dd, &d, sizeof(ObjDesc), hipMemcpyHostToDevice) == hipSuccess;
+  if (!ok) { cleanup(); return fail(ctx, "hipMemcpy failed (sdf_eval)"); }
+  const DevDecoder& D = dec->D;
+  hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)dz, (float*)db0, (float*)db4);
+  const int grid = std::min(ctx->n_cu, nt);
+  if (jac) {
+    GNParams P{};
+    hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+                       (const ObjDesc*)dd, (const ObjState*)nullptr, (const float*)nullptr,
+                       (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
+                       (float*)nullptr, (const float4*)dp, (float*)dout);
+  } else {
+    hipLaunchKernelGGL(k_mlp_fwd, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+                       (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout);
+  }
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    cleanup();
+    return fail(ctx, "kernel failed (sdf_eval)");
+  }
+  std::vector<float> h(outw * n);
+  ok = hipMemcpy(h.data(), dout, sizeof(float) * h.size(), hipMemcpyDeviceToHost) == hipSuccess;
+  cleanup();
+  if (!ok) return fail(ctx, "hipMemcpy D2H failed (sdf_eval)");
+  for (int i = 0; i < n; ++i) {
+    sdf[i] = h[i * outw];
+    if (jac)
+      for (int k = 0; k < IN; ++k) jac[(size_t)i * IN + k] = h[i * outw + 1 + k];
+  }
+  return 0;
+}
+
+int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, const float* t_co_se3,
+                  float scale, const float* pts, int n_pts, const float* code, float* t_out) {
+  (void)dec; (void)p; (void)t_co_se3; (void)scale; (void)pts; (void)n_pts; (void)code; (void)t_out;
+  return fail(ctx, "dsr_pose_only: not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// dsr_dev.hpp — device-side data layout shared by all libdsr kernels.
+//
+// Data layout in HBM (one batch of n_obj objects):
+//   pts   [sum n_pts][3]    surface points, camera frame          (input, resident)
+//   rays  [sum n_rays][3]   ray directions, fg first              (input, resident)
+//   dobs  [sum n_rays]      observed depth (fg) / 1.1*d_max (bg)   (input + per-iter)
+//   cand  [sum n_rays*M]    float4 (x,y,z, bits(ray*M+j)): ray samples inside the unit
+//                           ball, compacted in (ray, depth) order == torch.where order
+//   dense [sum n_rays*M]    SDF per (ray, depth) sample, NaN when outside the ball
+//   kpts  [sum n_rays*M]    float4 (x,y,z, de_ds) of the K render points
+//   kres  [sum n_rays*M]    clamped depth residual of the K render points
+//   slots [n_jac_tiles][SLOT_FLOATS] per-tile partial J^T J (upper tri), J^T r~, sum r~^2
+// Decoder weights are packed once into MFMA A-fragment order (see pack_frag in
+// dsr_api.hip) so each wave-instruction of a weight load reads 1 KiB contiguous.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dsr {
+
+constexpr int HID = 512;          // hidden width (dims=[512]*8)
+constexpr int CODE = 64;          // code_len
+constexpr int IN = CODE + 3;      // decoder input width
+constexpr int NPOSE = 7;          // Sim(3) tangent: rho(3) omega(3) s
+constexpr int NPAR = NPOSE + CODE;   // 71
+constexpr int NTRI = NPAR * (NPAR + 1) / 2;   // 2556 upper-triangle entries
+constexpr int SLOT_FLOATS = NTRI + NPAR + 1;  // + J^T r~ (71) + sum r~^2
+constexpr int TILE = 64;          // points per MLP tile
+constexpr int PITCH = 520;        // LDS row pitch (floats) of the [point][neuron] image:
+                                  // conflict-free ds_read_b128 for the B-fragment reads
+constexpr int NWAVE = 8;          // waves per MLP workgroup (512 threads)
+constexpr int MAXM = 64;          // max depth samples per ray
+constexpr int L3_OUT = 445;       // lin3 out (= 512 - 67, latent re-injection)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct DevDecoder {
+  const float4* Wf[8];   // forward A-fragments of lin1..lin7 (index = layer), [32 rb][K/16][64 lanes]
+  int Kf[8];             // padded K of each forward layer (512; 448 for lin4 = h3|xyz)
+  const float4* Wb[8];   // backward A-fragments of lin_l^T (l=1..7), Wb[0] = lin0^T (80 rows)
+  int Kb[8];             // K of each backward GEMM (512; 448 for lin3^T)
+  const float* bias[8];  // b_l padded to 512 (l = 0..7)
+  const float* W0x;      // [512][3]  lin0 xyz columns
+  const float* W0z;      // [512][64] lin0 code columns (folded into a per-object bias)
+  const float* W4z;      // [512][64] lin4 code columns (folded into a per-object bias)
+  const float* W8;       // [512]     lin8 row
+  float b8;
+};
+
+struct ObjDesc {
+  int pts_off, n_pts;    // into pts
+  int ray_off, n_rays;   // into rays / dobs
+  int n_fg;              // foreground rays (have observed depth)
+  int cand_off;          // into cand / dense / kpts / kres  (capacity n_rays*M)
+  int slot_sdf;          // first jac slot of this object's sdf tiles
+  int pad;
+};
+
+enum { ST_RUNNING = 0, ST_DONE = 1, ST_FAIL = 2 };
+
+struct ObjState {
+  float T[16];           // t_obj_cam (camera -> object), row-major
+  float Tco[16];         // inverse(T) of this iteration (optimizer.py:122)
+  float depths[MAXM];    // torch.linspace(d_min, d_max, M) (optimizer.py:126)
+  float dmin, dmax, delta_d, bg_depth;
+  float loss;            // returned loss (pre-update value of the last good iteration)
+  float sdf_loss, render_loss;
+  int status;            // ST_*
+  int fail_reason;       // DSR_FAIL_*
+  int iters_done;
+  int n_valid, k;        // this iteration's counts
+  int n_sdf_tiles, n_ren_tiles, slot_ren;   // this iteration's jac tiles
+  int pad[3];
+};
+
+struct Tile {
+  int obj, term, start, count;   // term: 0 = sdf (surface points), 1 = render (K list)
+};
+
+struct GNParams {
+  float k1, k2, k3, k4, b1, b2, lr, s_damp, cut_off;
+  int iters, M;
+};
+
+__device__ __forceinline__ float fetch4(const float4& v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+}  // namespace dsr

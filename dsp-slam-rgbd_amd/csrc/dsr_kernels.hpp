@@ -1,0 +1,894 @@
+// dsr_kernels.hpp — the device-resident Gauss-Newton iteration of
+// Optimizer.reconstruct_object (reconstruct/optimizer.py:90-205) for a batch of
+// independent objects.  One iteration = 8 launches, none of which needs the host:
+//
+//   k_iter_begin   optimizer.py:122-128  t_cam_obj, scale, linspace depths, bg depth,
+//                                        + code folded into lin0 / lin4 biases
+//   k_sample       loss.py:71-88         ray samples -> object frame -> |x|<1 ->
+//                                        ordered compaction (== torch.where order)
+//   k_tiles_fwd    —                     64-point tiles over every object's N_valid
+//   k_mlp_fwd      loss.py:91-92         decode_sdf on all in-ball samples (MFMA)
+//   k_render       loss.py:97-150        occupancy, transmittance cumprod, rendered
+//                                        depth, de_do, K-compaction, residual clamp
+//   k_tiles_jac    —                     tiles over N surface pts + K render pts
+//   k_mlp_jac      loss.py:22-43,157-164 fwd + analytic input Jacobian (MFMA), Sim(3)
+//                  loss_utils.py:176-195 point Jacobian, Huber (loss_utils.py:246-275),
+//                  optimizer.py:163-169  per-tile J^T J, J^T r~, sum r~^2
+//   k_solve        optimizer.py:131-194  reduce, damp, rotation prior, fp32 LU inverse,
+//                                        exp_sim3, pose/code update, failure exits
+#pragma once
+#include "dsr_dev.hpp"
+#include "dsr_mlp.hpp"
+#include "../../include/dsr.h"
+
+namespace dsr {
+
+// ------------------------------------------------------------------------------------
+// small fp32 linear algebra (single thread), mirroring torch CPU fp32 semantics
+// ------------------------------------------------------------------------------------
+// LU with partial pivoting (first max, LAPACK getrf), multipliers by reciprocal (sgetf2).
+template <int N>
+__device__ void lu_small(float (&a)[N][N], int (&piv)[N]) {
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+    float best = fabsf(a[k][k]);
+    for (int r = k + 1; r < N; ++r)
+      if (fabsf(a[r][k]) > best) { best = fabsf(a[r][k]); p = r; }
+    piv[k] = p;
+    if (p != k)
+      for (int c = 0; c < N; ++c) { float t = a[k][c]; a[k][c] = a[p][c]; a[p][c] = t; }
+    const float rc = 1.0f / a[k][k];
+    for (int r = k + 1; r < N; ++r) a[r][k] = a[r][k] * rc;
+    for (int r = k + 1; r < N; ++r)
+      for (int c = k + 1; c < N; ++c) a[r][c] = __builtin_fmaf(-a[r][k], a[k][c], a[r][c]);
+  }
+}
+
+template <int N>
+__device__ void inv_small(const float* m, float* out) {   // torch.inverse (getrf + getrs(I))
+  float a[N][N];
+  int piv[N];
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) a[i][j] = m[i * N + j];
+  lu_small<N>(a, piv);
+  for (int col = 0; col < N; ++col) {
+    float x[N];
+    for (int i = 0; i < N; ++i) x[i] = (i == col) ? 1.f : 0.f;
+    for (int k = 0; k < N; ++k)
+      if (piv[k] != k) { float t = x[k]; x[k] = x[piv[k]]; x[piv[k]] = t; }
+    for (int i = 0; i < N; ++i)
+      for (int l = 0; l < i; ++l) x[i] = __builtin_fmaf(-a[i][l], x[l], x[i]);
+    for (int i = N - 1; i >= 0; --i) {
+      for (int l = i + 1; l < N; ++l) x[i] = __builtin_fmaf(-a[i][l], x[l], x[i]);
+      x[i] = x[i] / a[i][i];
+    }
+    for (int i = 0; i < N; ++i) out[i * N + col] = x[i];
+  }
+}
+
+__device__ float det3(const float* m4 /*4x4, uses [:3,:3]*/) {   // torch.det via LU
+  float a[3][3];
+  int piv[3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) a[i][j] = m4[i * 4 + j];
+  lu_small<3>(a, piv);
+  float d = (a[0][0] * a[1][1]) * a[2][2];
+  int sw = (piv[0] != 0) + (piv[1] != 1);
+  return (sw & 1) ? -d : d;
+}
+
+__device__ void mm4(const float* A, const float* B, float* C) {
+  float t[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+      for (int k = 0; k < 4; ++k) s = s + A[i * 4 + k] * B[k * 4 + j];
+      t[i * 4 + j] = s;
+    }
+  for (int i = 0; i < 16; ++i) C[i] = t[i];
+}
+
+// exp_sim3 (loss_utils.py:198-243) in fp32, branch structure included
+// (theta<=1e-8 & s==0 / s!=0; c = 0 when s <= eps, also for negative s).
+__device__ void exp_sim3_dev(const float* x, float* out) {
+  const float v0 = x[0], v1 = x[1], v2 = x[2], w0 = x[3], w1 = x[4], w2 = x[5], s = x[6];
+  const float W[9] = {0.f, -w2, w1, w2, 0.f, -w0, -w1, w0, 0.f};
+  float W2[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      W2[i * 3 + j] = (W[i * 3 + 0] * W[0 * 3 + j] + W[i * 3 + 1] * W[1 * 3 + j]) + W[i * 3 + 2] * W[2 * 3 + j];
+  const float theta = sqrtf((w0 * w0 + w1 * w1) + w2 * w2);
+  const float t2 = theta * theta;
+  const float st = sinf(theta), ct = cosf(theta);
+  const float es = expf(s);
+  const float s2 = s * s;
+  float ew[9], J[9];
+  const float I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  if (theta <= 1e-8f) {
+    if (s == 0.f) {
+      for (int i = 0; i < 9; ++i) { ew[i] = I3[i]; J[i] = I3[i]; }
+    } else {
+      const float c = (es - 1.f) / s;
+      for (int i = 0; i < 9; ++i) { ew[i] = I3[i]; J[i] = c * I3[i]; }
+    }
+  } else {
+    for (int i = 0; i < 9; ++i) ew[i] = (I3[i] + W[i] * st / theta) + W2[i] * (1.f - ct) / t2;
+    const float a = es * st, b = es * ct;
+    const float c = (s <= 1e-8f) ? 0.f : (es - 1.f) / s;
+    const float k1 = (a * s + (1.f - b) * theta) / (s2 + t2);
+    const float k2 = c - ((b - 1.f) * s + a * theta) / (s2 + t2);
+    for (int i = 0; i < 9; ++i) J[i] = (c * I3[i] + k1 * W[i] / theta) + k2 * W2[i] / t2;
+  }
+  for (int i = 0; i < 16; ++i) out[i] = (i % 5 == 0) ? 1.f : 0.f;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) out[i * 4 + j] = es * ew[i * 3 + j];
+    out[i * 4 + 3] = (J[i * 3 + 0] * v0 + J[i * 3 + 1] * v1) + J[i * 3 + 2] * v2;
+  }
+}
+
+// (p[...,None,:] * T[:3,:3]).sum(-1) + T[:3,3]   (loss.py:31-32, :74-77)
+__device__ __forceinline__ float3 xform(const float* T, float x, float y, float z) {
+  float3 o;
+  o.x = ((x * T[0] + y * T[1]) + z * T[2]) + T[3];
+  o.y = ((x * T[4] + y * T[5]) + z * T[6]) + T[7];
+  o.z = ((x * T[8] + y * T[9]) + z * T[10]) + T[11];
+  return o;
+}
+
+// ------------------------------------------------------------------------------------
+// state init / per-iteration prologue
+// ------------------------------------------------------------------------------------
+__global__ void k_init_state(int n_obj, const float* __restrict__ t_in, const int* __restrict__ is_oc,
+                             const float* __restrict__ z_in, ObjState* st, float* zbuf) {
+  const int o = blockIdx.x;
+  if (o >= n_obj) return;
+  if (threadIdx.x < CODE) zbuf[o * CODE + threadIdx.x] = z_in[o * CODE + threadIdx.x];
+  if (threadIdx.x == 0) {
+    ObjState& S = st[o];
+    if (is_oc[o]) {
+      for (int i = 0; i < 16; ++i) S.T[i] = t_in[o * 16 + i];
+    } else {
+      inv_small<4>(t_in + o * 16, S.T);      // optimizer.py:105-106
+    }
+    S.loss = 0.f;                              // optimizer.py:119
+    S.status = ST_RUNNING;
+    S.fail_reason = 0;
+    S.iters_done = 0;
+    S.n_valid = S.k = 0;
+    S.sdf_loss = S.render_loss = 0.f;
+  }
+}
+
+// optimizer.py:122-128 and the code fold of lin0 / lin4.
+__global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
+                             const float* __restrict__ zbuf, DevDecoder D, GNParams P,
+                             float* __restrict__ bias0f, float* __restrict__ bias4f,
+                             float* __restrict__ dobs) {
+  const int o = blockIdx.x;
+  ObjState& S = st[o];
+  if (S.status != ST_RUNNING) return;
+  const int tid = threadIdx.x;
+  __shared__ float z[CODE];
+  if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
+  __syncthreads();
+  for (int n = tid; n < HID; n += blockDim.x) {
+    float s0 = 0.f, s4 = 0.f;
+    for (int k = 0; k < CODE; ++k) {
+      s0 = __builtin_fmaf(D.W0z[n * CODE + k], z[k], s0);
+      s4 = __builtin_fmaf(D.W4z[n * CODE + k], z[k], s4);
+    }
+    bias0f[o * HID + n] = D.bias[0][n] + s0;
+    bias4f[o * HID + n] = D.bias[4][n] + s4;
+  }
+  if (tid == 0) {
+    inv_small<4>(S.T, S.Tco);                                  // :122
+    const float scale = powf(det3(S.Tco), 0.33333334f);        // :123 det ** (1/3)
+    const float dmin = S.Tco[11] - 1.0f * scale;               // :124
+    const float dmax = S.Tco[11] + 1.0f * scale;
+    const int M = P.M;
+    const float step = (dmax - dmin) / (float)(M - 1);         // torch.linspace (CPU, fp32)
+    const int half = M / 2;
+    for (int i = 0; i < M; ++i)
+      S.depths[i] = (i < half) ? __builtin_fmaf(step, (float)i, dmin)
+                               : __builtin_fmaf(-step, (float)(M - 1 - i), dmax);
+    S.dmin = S.depths[0];
+    S.dmax = S.depths[M - 1];
+    S.delta_d = (S.depths[M - 1] - S.depths[0]) / (float)(M - 1);   // loss.py:140
+    S.bg_depth = 1.1f * dmax;                                  // :128
+    S.n_valid = 0;
+    S.k = 0;
+  }
+  __syncthreads();
+  const ObjDesc d = desc[o];
+  const float bg = S.bg_depth;
+  for (int r = d.n_fg + tid; r < d.n_rays; r += blockDim.x) dobs[d.ray_off + r] = bg;
+}
+
+// ------------------------------------------------------------------------------------
+// k_sample: ray samples -> object frame -> |x| < 1 -> ordered compaction
+// ------------------------------------------------------------------------------------
+constexpr int SAMPLE_THREADS = 1024;
+
+__device__ __forceinline__ float3 ray_sample(const float* __restrict__ rays, const ObjState& S,
+                                             int ray, int j) {
+  const float d = S.depths[j];
+  const float cx = rays[ray * 3 + 0] * d, cy = rays[ray * 3 + 1] * d, cz = rays[ray * 3 + 2] * d;
+  return xform(S.T, cx, cy, cz);
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(int n_obj, const ObjDesc* __restrict__ desc,
+                                                           ObjState* st, const float* __restrict__ rays_all,
+                                                           int M, float4* __restrict__ cand,
+                                                           float* __restrict__ dense) {
+  const int o = blockIdx.x;
+  ObjState& S = st[o];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[o];
+  const float* rays = rays_all + (size_t)d.ray_off * 3;
+  const int total = d.n_rays * M;
+  __shared__ int wsum[SAMPLE_THREADS / 64];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < total; c0 += SAMPLE_THREADS) {
+    const int c = c0 + tid;
+    bool valid = false;
+    float3 x = make_float3(0.f, 0.f, 0.f);
+    if (c < total) {
+      const int ray = c / M, j = c - (c / M) * M;
+      x = ray_sample(rays, S, ray, j);
+      const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+      valid = nrm < 1.0f;                                              // loss.py:82
+      if (!valid) dense[d.cand_off + c] = __builtin_nanf("");
+    }
+    const uint64_t bal = __ballot(valid);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int off = base_s;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
+    if (valid)
+      cand[d.cand_off + off + before] = make_float4(x.x, x.y, x.z, __int_as_float(c));
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int k = 0; k < SAMPLE_THREADS / 64; ++k) t += wsum[k];
+      base_s += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    S.n_valid = base_s;
+    if (base_s < 10) {                        // loss.py:86-88 -> optimizer.py:144-145
+      S.status = ST_FAIL;
+      S.fail_reason = DSR_FAIL_RENDER_FEW;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// tile tables (single workgroup)
+// ------------------------------------------------------------------------------------
+__global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+  __shared__ int base_s;
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  for (int o = 0; o < n_obj; ++o) {
+    const ObjState& S = st[o];
+    const int n = (S.status == ST_RUNNING) ? S.n_valid : 0;
+    const int nt = (n + TILE - 1) / TILE;
+    const int b = base_s;
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+      Tile t;
+      t.obj = o; t.term = 0; t.start = i * TILE;
+      t.count = min(TILE, n - i * TILE);
+      tiles[b + i] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) base_s = b + nt;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_tiles = base_s;
+}
+
+__global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+  __shared__ int base_s;
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  for (int o = 0; o < n_obj; ++o) {
+    ObjState& S = st[o];
+    const bool run = S.status == ST_RUNNING;
+    const int ns = run ? desc[o].n_pts : 0;
+    const int nk = run ? S.k : 0;
+    const int ts = (ns + TILE - 1) / TILE, tk = (nk + TILE - 1) / TILE;
+    const int b = base_s;
+    for (int i = threadIdx.x; i < ts + tk; i += blockDim.x) {
+      Tile t;
+      t.obj = o;
+      if (i < ts) { t.term = 0; t.start = i * TILE; t.count = min(TILE, ns - i * TILE); }
+      else { const int j = i - ts; t.term = 1; t.start = j * TILE; t.count = min(TILE, nk - j * TILE); }
+      tiles[b + i] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      base_s = b + ts + tk;
+      S.n_sdf_tiles = ts;
+      S.n_ren_tiles = tk;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *n_tiles = base_s;
+}
+
+// ------------------------------------------------------------------------------------
+// k_mlp_fwd: decode_sdf over every in-ball ray sample (persistent, one tile per pass)
+// ------------------------------------------------------------------------------------
+struct FwdShared {
+  float H[H_FLOATS];
+  float xyz[TILE * 4];
+  float red[NWAVE * TILE];
+};
+
+__global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __restrict__ tiles,
+                                                 const int* __restrict__ n_tiles,
+                                                 const ObjDesc* __restrict__ desc,
+                                                 const float4* __restrict__ cand,
+                                                 const float* __restrict__ bias0f,
+                                                 const float* __restrict__ bias4f,
+                                                 float* __restrict__ dense) {
+  __shared__ FwdShared sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = *n_tiles;
+  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+    const Tile tl = tiles[ti];
+    const ObjDesc d = desc[tl.obj];
+    const float4* src = cand + d.cand_off + tl.start;
+    if (tid < TILE) {
+      float4 v = (tid < tl.count) ? src[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+      sm.xyz[tid * 4 + 0] = v.x; sm.xyz[tid * 4 + 1] = v.y;
+      sm.xyz[tid * 4 + 2] = v.z; sm.xyz[tid * 4 + 3] = v.w;
+    }
+    __syncthreads();
+    uint64_t mask;
+    layer0_fwd(D, bias0f + tl.obj * HID, sm.xyz, sm.H, w, lane, mask);
+    __syncthreads();
+    floatx4 acc[4][4];
+    for (int l = 1; l <= 6; ++l) {
+      const int T = D.Kf[l] / 16;
+      gemm_tile<4>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      __syncthreads();
+      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mask, l == 3);
+      __syncthreads();
+    }
+    {
+      const int T = D.Kf[7] / 16;
+      gemm_tile<4>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      epi_l7(acc, D, sm.red, w, lane, mask);
+    }
+    __syncthreads();
+    if (tid < tl.count) {
+      float s = sm.red[tid];
+      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+      const float y = tanhf(s + D.b8);
+      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
+      dense[d.cand_off + idx] = y;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_render: per-ray occupancy scan (loss.py:97-150), one workgroup per object
+// ------------------------------------------------------------------------------------
+constexpr int RENDER_THREADS = 128;
+
+__global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjDesc* __restrict__ desc,
+                                                           ObjState* st, const float* __restrict__ rays_all,
+                                                           const float* __restrict__ dobs_all, GNParams P,
+                                                           const float* __restrict__ dense,
+                                                           float4* __restrict__ kpts,
+                                                           float* __restrict__ kres) {
+  const int o = blockIdx.x;
+  ObjState& S = st[o];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[o];
+  const int M = P.M;
+  const float th = P.cut_off;
+  const float nth = -th, two_th = 2.0f * th;
+  const float do_ds = (float)(-1.0 / (2.0 * (double)th));
+  const float* rays = rays_all + (size_t)d.ray_off * 3;
+  __shared__ float occ_s[RENDER_THREADS * (MAXM + 1)];
+  __shared__ float T_s[RENDER_THREADS * (MAXM + 1)];
+  __shared__ int cnt_s[RENDER_THREADS];
+  __shared__ int base_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  const float dmax = S.dmax, delta_d = S.delta_d;
+  float* occ = occ_s + tid * (MAXM + 1);
+  float* Tr = T_s + tid * (MAXM + 1);
+  for (int r0 = 0; r0 < d.n_rays; r0 += RENDER_THREADS) {
+    const int ray = r0 + tid;
+    int cnt = 0;
+    float du = 0.f, dob = 0.f;
+    uint64_t grad = 0;
+    if (ray < d.n_rays) {
+      const float* sd = dense + d.cand_off + (size_t)ray * M;
+      for (int j = 0; j < M; ++j) {
+        const float s = sd[j];
+        float ov = 0.f;
+        if (!(s != s)) {                              // valid sample (dense holds NaN outside)
+          const float cl = fminf(fmaxf(s, nth), th);
+          ov = 0.5f - cl / two_th;                    // sdf_to_occupancy (loss_utils.py:40-48)
+          if (s > nth && s < th) grad |= 1ull << j;   // loss.py:101
+        }
+        occ[j] = ov;
+      }
+      // cumprod of (1 - o) (loss.py:111), term probabilities, rendered depth (:112-125)
+      float T = 1.f;
+      for (int j = 0; j < M; ++j) {
+        const float tp = occ[j] * T;
+        T = T * (1.f - occ[j]);
+        Tr[j] = T;
+        du = du + S.depths[j] * tp;
+      }
+      du = du + (1.1f * dmax) * T;                   // background bin o=1, d=1.1*d_max
+      dob = dobs_all[d.ray_off + ray];
+      for (uint64_t m = grad; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        float sacc = 0.f;
+        for (int l = j; l < M; ++l) sacc = sacc + Tr[l];
+        const float dedo = sacc / (1.f - occ[j]);     // :131-132
+        if (dedo > 1e-2f) ++cnt;                      // :135
+      }
+    }
+    cnt_s[tid] = cnt;
+    __syncthreads();
+    int off = base_s;
+    for (int k = 0; k < tid; ++k) off += cnt_s[k];
+    if (cnt > 0) {
+      float res = dob - du;                           // :145
+      res = res > 0.30f ? 0.30f : res;                // :147-148
+      res = res < -0.30f ? -0.30f : res;
+      for (uint64_t m = grad; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        float sacc = 0.f;
+        for (int l = j; l < M; ++l) sacc = sacc + Tr[l];
+        const float dedo = sacc / (1.f - occ[j]);
+        if (dedo > 1e-2f) {
+          const float deds = (dedo * delta_d) * do_ds;  // :142
+          const float3 x = ray_sample(rays, S, ray, j);
+          kpts[d.cand_off + off] = make_float4(x.x, x.y, x.z, deds);
+          kres[d.cand_off + off] = res;
+          ++off;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == RENDER_THREADS - 1) base_s = off;   // = base + sum of this chunk's counts
+    __syncthreads();
+  }
+  if (tid == 0) S.k = base_s;
+}
+
+// ------------------------------------------------------------------------------------
+// k_mlp_jac: forward + analytic input Jacobian + per-tile normal-equation partials
+// ------------------------------------------------------------------------------------
+struct JacShared {
+  float H[H_FLOATS];           // activations / gradients, later the tile's J [64][72]
+  float xyz[TILE * 4];         // object-frame point (x,y,z) + de_ds (render term)
+  float red[NWAVE * TILE];     // lin8 partials
+  float y[TILE];               // sdf
+  float r[TILE];               // raw residual (render) ; later r~ (Huber-weighted)
+  float gin[TILE * GIN_PITCH]; // d sdf / d [code(64), xyz(3)]
+};
+
+constexpr int JPITCH = 72;
+
+__global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __restrict__ tiles,
+                                                 const int* __restrict__ n_tiles,
+                                                 const ObjDesc* __restrict__ desc,
+                                                 const ObjState* __restrict__ st,
+                                                 const float* __restrict__ pts_all,
+                                                 const float4* __restrict__ kpts,
+                                                 const float* __restrict__ kres,
+                                                 const float* __restrict__ bias0f,
+                                                 const float* __restrict__ bias4f, GNParams P,
+                                                 float* __restrict__ slots,
+                                                 const float4* __restrict__ raw_pts,
+                                                 float* __restrict__ raw_out) {
+  __shared__ JacShared sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = *n_tiles;
+  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+    const Tile tl = tiles[ti];
+    const ObjDesc d = desc[tl.obj];
+    // ---- load points
+    if (tid < TILE) {
+      float x = 0.f, y = 0.f, z = 0.f, aux = 0.f, rr = 0.f;
+      if (tid < tl.count) {
+        if (tl.term == 0) {                          // surface points -> object frame (loss.py:31-32)
+          const float* p = pts_all + (size_t)(d.pts_off + tl.start + tid) * 3;
+          const float3 xo = xform(st[tl.obj].T, p[0], p[1], p[2]);
+          x = xo.x; y = xo.y; z = xo.z;
+        } else if (tl.term == 1) {
+          const float4 v = kpts[d.cand_off + tl.start + tid];
+          x = v.x; y = v.y; z = v.z; aux = v.w;
+          rr = kres[d.cand_off + tl.start + tid];
+        } else {
+          const float4 v = raw_pts[tl.start + tid];
+          x = v.x; y = v.y; z = v.z;
+        }
+      }
+      sm.xyz[tid * 4 + 0] = x; sm.xyz[tid * 4 + 1] = y;
+      sm.xyz[tid * 4 + 2] = z; sm.xyz[tid * 4 + 3] = aux;
+      sm.r[tid] = rr;
+    }
+    __syncthreads();
+    // ---- forward, masks kept in registers
+    uint64_t mk[8];
+    layer0_fwd(D, bias0f + tl.obj * HID, sm.xyz, sm.H, w, lane, mk[0]);
+    __syncthreads();
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int l = 1; l <= 6; ++l) {
+      const int T = D.Kf[l] / 16;
+      gemm_tile<4>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      __syncthreads();
+      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mk[l], l == 3);
+      __syncthreads();
+    }
+    {
+      const int T = D.Kf[7] / 16;
+      gemm_tile<4>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      epi_l7(acc, D, sm.red, w, lane, mk[7]);
+    }
+    __syncthreads();
+    if (tid < TILE) {
+      float s = sm.red[tid];
+      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+      sm.y[tid] = tanhf(s + D.b8);
+    }
+    __syncthreads();
+    // ---- g7 = (1 - y^2) W8 (.) relu'(a7)  (tanh backward, lin8 backward)
+    {
+      const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 w8 = *reinterpret_cast<const float4*>(D.W8 + n0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
+          const float yy = sm.y[p];
+          const float dt = 1.f - yy * yy;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[r] = ((mk[7] >> ((q * 4 + cb) * 4 + r)) & 1ull) ? dt * fetch4(w8, r) : 0.f;
+          *reinterpret_cast<float4*>(sm.H + p * PITCH + n0) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- backward GEMMs: lin7^T .. lin1^T
+#pragma unroll
+    for (int l = 7; l >= 1; --l) {
+      const int T = D.Kb[l] / 16;
+      gemm_tile<4>(D.Wb[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      __syncthreads();
+      if (l == 4) epi_bwd_l4(acc, sm.H, sm.gin, w, lane, mk[3]);
+      else epi_bwd(acc, sm.H, w, lane, mk[l - 1]);
+      __syncthreads();
+    }
+    // ---- lin0^T: d sdf / d input (67 rows) = W0^T g0 + skip part (already in gin)
+    if (w < 5) {
+      floatx4 a1[1][4];
+      gemm_tile<1>(D.Wb[0] + (size_t)w * 32 * 64, 32, sm.H, a1, lane);
+      const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int p = 16 * cb + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * w + 4 * g + r;
+          if (n < IN) sm.gin[p * GIN_PITCH + n] = accr(a1[0][cb], r) + sm.gin[p * GIN_PITCH + n];
+        }
+      }
+    }
+    __syncthreads();
+    if (tl.term == 2) {            // raw query (dsr_sdf_eval): sdf + gradient out
+      for (int e = tid; e < TILE * (IN + 1); e += 512) {
+        const int p = e / (IN + 1), k = e - p * (IN + 1);
+        if (p < tl.count)
+          raw_out[(size_t)(tl.start + p) * (IN + 1) + k] = (k == 0) ? sm.y[p] : sm.gin[p * GIN_PITCH + k - 1];
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- J rows (loss.py:34-41 / :157-164) into the freed H region
+    float* J = sm.H;
+    {
+      const int p = tid >> 3, sub = tid & 7;
+      const bool valid = p < tl.count;
+      const bool ren = tl.term == 1;
+      const float deds = sm.xyz[p * 4 + 3];
+      const float* gi = sm.gin + p * GIN_PITCH;
+      for (int e = sub; e < NPAR; e += 8) {
+        float v;
+        if (e >= NPOSE) {
+          v = ren ? deds * gi[e - NPOSE] : gi[e - NPOSE];
+        } else {
+          const float g0 = ren ? deds * gi[64] : gi[64];
+          const float g1 = ren ? deds * gi[65] : gi[65];
+          const float g2 = ren ? deds * gi[66] : gi[66];
+          const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
+          // g . [I | -[x]x | x]  (get_points_to_pose_jacobian_sim3, loss_utils.py:176-195)
+          switch (e) {
+            case 0: v = g0; break;
+            case 1: v = g1; break;
+            case 2: v = g2; break;
+            case 3: v = g1 * (-z) + g2 * y; break;
+            case 4: v = g0 * z + g2 * (-x); break;
+            case 5: v = g0 * (-y) + g1 * x; break;
+            default: v = (g0 * x + g1 * y) + g2 * z; break;
+          }
+        }
+        J[p * JPITCH + e] = valid ? v : 0.f;
+      }
+      if (tid < TILE) {
+        // Huber-weighted residual (loss_utils.py:246-275); sdf residual = decoder output
+        const float res = ren ? sm.r[tid] : sm.y[tid];
+        const float b = ren ? P.b1 : P.b2;
+        const float x = fabsf(res);
+        const float hn = (x <= b) ? x * x : (2.0f * b) * x - b * b;
+        const float den = (x == 0.f) ? 1.f : x;
+        const float wgt = sqrtf(hn) / den;
+        sm.r[tid] = (tid < tl.count) ? wgt * res : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- per-tile partials: upper-tri J^T J, J^T r~, sum r~^2
+    {
+      const int slot = d.slot_sdf + (tl.term == 0 ? 0 : st[tl.obj].n_sdf_tiles) + tl.start / TILE;
+      float* out = slots + (size_t)slot * SLOT_FLOATS;
+      for (int e = tid; e < SLOT_FLOATS; e += 512) {
+        float s = 0.f;
+        if (e < NTRI) {
+          int a = 0, rem = e;
+          while (rem >= NPAR - a) { rem -= NPAR - a; ++a; }
+          const int b = a + rem;
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], J[p * JPITCH + b], s);
+        } else if (e < NTRI + NPAR) {
+          const int a = e - NTRI;
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], sm.r[p], s);
+        } else {
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(sm.r[p], sm.r[p], s);
+        }
+        out[e] = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_solve: optimizer.py:131-194 for one object per workgroup
+// ------------------------------------------------------------------------------------
+constexpr int SOLVE_THREADS = 256;
+constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render, T, z
+
+__global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDesc* __restrict__ desc,
+                                                         ObjState* st, float* __restrict__ zbuf,
+                                                         GNParams P, const float* __restrict__ slots,
+                                                         float* __restrict__ trace_H,
+                                                         float* __restrict__ trace_v,
+                                                         int* __restrict__ trace_i) {
+  const int o = blockIdx.x;
+  ObjState& S = st[o];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[o];
+  const int tid = threadIdx.x;
+  __shared__ float Ss[SLOT_FLOATS];
+  __shared__ float Sr[SLOT_FLOATS];
+  __shared__ float A[NPAR][NPAR + 1];
+  __shared__ float X[NPAR][NPAR + 1];
+  __shared__ float bv[NPAR], dx[NPAR], z[CODE];
+  __shared__ float jrot[NPOSE];
+  __shared__ float scal[4];
+  __shared__ int piv[NPAR];
+  __shared__ int flag;
+  const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
+  for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {
+    float a = 0.f, b = 0.f;
+    for (int t = 0; t < ns; ++t) a += slots[(size_t)(d.slot_sdf + t) * SLOT_FLOATS + e];
+    for (int t = 0; t < nk; ++t) b += slots[(size_t)(d.slot_sdf + ns + t) * SLOT_FLOATS + e];
+    Ss[e] = a;
+    Sr[e] = b;
+  }
+  if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
+  __syncthreads();
+  const int it = S.iters_done;
+  if (tid == 0) {
+    const float N = (float)d.n_pts, K = (float)S.k;
+    const float sdf_loss = Ss[SLOT_FLOATS - 1] / N;
+    const float ren_loss = Sr[SLOT_FLOATS - 1] / K;     // K == 0 -> NaN, like mean(empty)
+    S.sdf_loss = sdf_loss;
+    S.render_loss = ren_loss;
+    int f = 0;
+    if (sdf_loss != sdf_loss) f = DSR_FAIL_SDF_NAN;                 // optimizer.py:137
+    else if (ren_loss != ren_loss) f = DSR_FAIL_RENDER_NAN;         // :151
+    flag = f;
+    if (f) {
+      S.status = ST_FAIL;
+      S.fail_reason = f;
+    } else {
+      scal[0] = P.k1 * ren_loss + P.k2 * sdf_loss;                 // :157
+      // rotation prior, loss.py:169-192, at the current (pre-update) pose
+      float rco[16];
+      for (int i = 0; i < 16; ++i) rco[i] = S.Tco[i];
+      const float sc = powf(det3(rco), 0.33333334f);
+      float r3[9], roc[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r3[i * 3 + j] = rco[i * 4 + j] / sc;
+      inv_small<3>(r3, roc);
+      const float res_rot = 1.f - (-r3[1 * 3 + 1]);              // 1 - (R_co e_y).n_g
+      for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
+      if (res_rot < 1e-7f) {
+        scal[1] = 0.f;
+      } else {
+        jrot[3] = roc[2 * 3 + 1];                                   // (R_oc n_g) x e_y
+        jrot[4] = 0.f;
+        jrot[5] = -roc[0 * 3 + 1];
+        scal[1] = res_rot;
+      }
+      scal[2] = N;
+      scal[3] = K;
+    }
+  }
+  __syncthreads();
+  if (flag) return;
+  // ---- H, b (optimizer.py:161-186)
+  {
+    const float N = scal[2], K = scal[3];
+    const float k1 = P.k1, k2 = P.k2, k3 = P.k3, k4 = P.k4;
+    for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) {
+      const int a = e / NPAR, b = e - (e / NPAR) * NPAR;
+      const int lo = min(a, b), hi = max(a, b);
+      const int idx = lo * NPAR - lo * (lo - 1) / 2 + (hi - lo);
+      float h = (k1 * Sr[idx]) / K + (k2 * Ss[idx]) / N;
+      if (a >= NPOSE && a == b) h = h + k3;
+      if (a < NPOSE && b < NPOSE) {
+        h = h + k4 * (jrot[a] * jrot[b]);
+        if (a == b) h = h + 1.f;
+        if (a == NPOSE - 1 && b == NPOSE - 1) h = h + P.s_damp;
+      }
+      A[a][b] = h;
+    }
+    for (int a = tid; a < NPAR; a += SOLVE_THREADS) {
+      float v = ((-k1) * Sr[NTRI + a]) / K + ((-k2) * Ss[NTRI + a]) / N;
+      if (a >= NPOSE) v = v - k3 * z[a - NPOSE];
+      else v = v - k4 * (-(jrot[a] * scal[1]));
+      bv[a] = v;
+    }
+  }
+  __syncthreads();
+  if (trace_H) {
+    for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS)
+      trace_H[((size_t)it * n_obj + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
+  }
+  __syncthreads();
+  // ---- LU with partial pivoting (torch.inverse, optimizer.py:188)
+  for (int k = 0; k < NPAR; ++k) {
+    if (tid < 64) {
+      float best = -1.f;
+      int bi = NPAR;
+      for (int r = k + tid; r < NPAR; r += 64) {
+        const float v = fabsf(A[r][k]);
+        if (v > best) { best = v; bi = r; }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (tid == 0) piv[k] = bi;
+    }
+    __syncthreads();
+    const int p = piv[k];
+    if (p != k)
+      for (int c = tid; c < NPAR; c += SOLVE_THREADS) { float t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+    __syncthreads();
+    const float rc = 1.0f / A[k][k];
+    for (int r = k + 1 + tid; r < NPAR; r += SOLVE_THREADS) A[r][k] = A[r][k] * rc;
+    __syncthreads();
+    const int m = NPAR - k - 1;
+    for (int e = tid; e < m * m; e += SOLVE_THREADS) {
+      const int r = k + 1 + e / m, c = k + 1 + e % m;
+      A[r][c] = __builtin_fmaf(-A[r][k], A[k][c], A[r][c]);
+    }
+    __syncthreads();
+  }
+  if (tid < NPAR) {                     // column tid of inverse(H)
+    const int col = tid;
+    float x[NPAR];
+    for (int i = 0; i < NPAR; ++i) x[i] = (i == col) ? 1.f : 0.f;
+    for (int k = 0; k < NPAR; ++k) {
+      const int p = piv[k];
+      if (p != k) { float t = x[k]; x[k] = x[p]; x[p] = t; }
+    }
+    for (int i = 0; i < NPAR; ++i)
+      for (int l = 0; l < i; ++l) x[i] = __builtin_fmaf(-A[i][l], x[l], x[i]);
+    for (int i = NPAR - 1; i >= 0; --i) {
+      for (int l = i + 1; l < NPAR; ++l) x[i] = __builtin_fmaf(-A[i][l], x[l], x[i]);
+      x[i] = x[i] / A[i][i];
+    }
+    for (int i = 0; i < NPAR; ++i) X[i][col] = x[i];
+  }
+  __syncthreads();
+  if (tid < NPAR) {                     // dx = inverse(H) b
+    float s = 0.f;
+    for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
+    dx[tid] = s;
+  }
+  __syncthreads();
+  if (tid < CODE) zbuf[o * CODE + tid] = z[tid] + P.lr * dx[NPOSE + tid];   // :194
+  if (tid == 0) {
+    float xi[NPOSE], dT[16], Tn[16], Tprev[16];
+    for (int i = 0; i < 16; ++i) Tprev[i] = S.T[i];
+    for (int i = 0; i < NPOSE; ++i) xi[i] = P.lr * dx[i];
+    exp_sim3_dev(xi, dT);                                         // :190
+    mm4(dT, S.T, Tn);                                             // :192
+    for (int i = 0; i < 16; ++i) S.T[i] = Tn[i];
+    S.loss = scal[0];
+    S.iters_done = it + 1;
+    if (it + 1 >= P.iters) S.status = ST_DONE;
+    if (trace_v) {
+      float* tv = trace_v + ((size_t)it * n_obj + o) * TRACE_V;
+      for (int i = 0; i < NPAR; ++i) { tv[i] = bv[i]; tv[NPAR + i] = dx[i]; }
+      tv[2 * NPAR + 0] = scal[0];
+      tv[2 * NPAR + 1] = S.sdf_loss;
+      tv[2 * NPAR + 2] = S.render_loss;
+      for (int i = 0; i < 16; ++i) tv[2 * NPAR + 3 + i] = Tprev[i];
+      for (int i = 0; i < CODE; ++i) tv[2 * NPAR + 19 + i] = z[i];
+    }
+  }
+  if (trace_i && tid == 0) {
+    trace_i[((size_t)it * n_obj + o) * 2 + 0] = S.n_valid;
+    trace_i[((size_t)it * n_obj + o) * 2 + 1] = S.k;
+  }
+}
+
+// per-iteration counters for the algorithmic-FLOP bookkeeping
+__global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
+                        int it, int* __restrict__ counts) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n_obj) return;
+  const ObjState& S = st[o];
+  counts[((size_t)it * n_obj + o) * 2 + 0] = S.n_valid;
+  counts[((size_t)it * n_obj + o) * 2 + 1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
+}
+
+__global__ void k_finalize(int n_obj, const ObjState* __restrict__ st, const float* __restrict__ zbuf,
+                           dsr_object_out* __restrict__ out) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n_obj) return;
+  const ObjState& S = st[o];
+  dsr_object_out r;
+  r.is_good = (S.status == ST_DONE) ? 1 : 0;
+  r.fail_reason = S.fail_reason;
+  r.loss = S.loss;
+  r.iters_done = S.iters_done;
+  r.n_valid_last = S.n_valid;
+  r.k_last = S.k;
+  inv_small<4>(S.T, r.t_cam_obj);                                  // optimizer.py:202
+  for (int i = 0; i < CODE; ++i) r.code[i] = zbuf[o * CODE + i];
+  out[o] = r;
+}
+
+}  // namespace dsr

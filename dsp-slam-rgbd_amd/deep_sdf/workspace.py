@@ -1,0 +1,130 @@
+"""DeepSDF checkpoint loader — the weight-format boundary of the hot path.
+
+Replaces ``deep_sdf/workspace.py:202-223`` (``config_decoder``): reads the same
+``specs.json`` + ``ModelParameters/<checkpoint>.pth`` (``model_state_dict`` with
+``module.lin{i}.weight_g / weight_v / bias`` keys, workspace.py:214-218), folds
+weight normalisation exactly as the reference module does at forward time
+(``torch._weight_norm(v, g, 0)``, i.e. ``nn.utils.weight_norm``'s hook) so the
+effective fp32 weights are bit-identical, and uploads them once into libdsr's
+MFMA fragment layout.  The checkpoint is read with ``torch.load(weights_only=True)``
+only.  PyTorch is plumbing here (file format + the fold), never compute.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+
+model_params_subdir = "ModelParameters"
+specifications_filename = "specs.json"
+
+
+def load_specs(experiment_directory):
+    fn = os.path.join(experiment_directory, specifications_filename)
+    if not os.path.isfile(fn):
+        raise Exception('The experiment directory does not include specifications file "specs.json"')
+    with open(fn) as f:
+        return json.load(f)
+
+
+def fold_state(state_dict, specs):
+    """Effective (W, b) per ``lin{i}`` as fp32 numpy arrays, computed with torch's own
+    weight-norm op (same kernel the reference's hook runs)."""
+    import torch
+
+    sd = {}
+    for k, v in state_dict.items():
+        k = k[len("module."):] if k.startswith("module.") else k
+        sd[k] = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))
+    layers = []
+    i = 0
+    while f"lin{i}.bias" in sd:
+        if f"lin{i}.weight_v" in sd:
+            W = torch._weight_norm(sd[f"lin{i}.weight_v"].float(), sd[f"lin{i}.weight_g"].float(), 0)
+        else:
+            W = sd[f"lin{i}.weight"].float()
+        layers.append((W.detach().cpu().numpy().astype(np.float32),
+                       sd[f"lin{i}.bias"].float().detach().cpu().numpy().astype(np.float32)))
+        i += 1
+    if not layers:
+        raise ValueError("checkpoint holds no lin{i} layers")
+    return layers
+
+
+def check_topology(specs, layers):
+    """Reject decoder variants libdsr does not implement (loudly, never approximated)."""
+    ns = specs["NetworkSpecs"]
+    if not ns.get("weight_norm", False):
+        raise NotImplementedError("LayerNorm DeepSDF decoders (weight_norm=False, "
+                                  "deep_sdf_decoder.py:58-63) are not supported by libdsr")
+    if ns.get("xyz_in_all"):
+        raise NotImplementedError("xyz_in_all decoders are not supported by libdsr")
+    if ns.get("use_tanh"):
+        raise NotImplementedError("use_tanh decoders are not supported by libdsr")
+    if list(ns.get("latent_in", [])) != [4]:
+        raise NotImplementedError("libdsr supports latent_in=[4] only")
+    if specs["CodeLength"] != 64:
+        raise NotImplementedError("libdsr supports CodeLength=64 only")
+    shapes = [W.shape for W, _ in layers]
+    want = [(512, 67)] + [(512, 512)] * 2 + [(445, 512)] + [(512, 512)] * 4 + [(1, 512)]
+    if shapes != want:
+        raise NotImplementedError(f"unsupported decoder shapes {shapes}")
+
+
+class Decoder:
+    """Device-resident DeepSDF decoder handle (what ``get_decoder`` returns).
+
+    Mirrors what the reference's callers use of the module: it is passed to
+    ``Optimizer`` / ``MeshExtractor``; ``code_len`` and ``layers`` are informative.
+    """
+
+    def __init__(self, specs, layers, device=None):
+        import ctypes as C
+
+        from reconstruct import _libdsr as L
+
+        check_topology(specs, layers)
+        self.specs = specs
+        self.code_len = specs["CodeLength"]
+        self.layers = layers
+        self.ctx = L.Context.get(device)
+        desc = L.DecoderDesc()
+        desc.code_len = self.code_len
+        desc.n_layers = len(layers)
+        for i, (W, _) in enumerate(layers):
+            desc.out_dim[i], desc.in_dim[i] = W.shape
+        desc.latent_in = 4
+        desc.use_tanh = 0
+        desc.xyz_in_all = 0
+        flat = np.concatenate([np.concatenate([W.reshape(-1), b.reshape(-1)]) for W, b in layers])
+        self._flat = np.ascontiguousarray(flat, np.float32)
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.lib.dsr_decoder_load(self.ctx.handle, C.byref(desc),
+                                                     L.fptr(self._flat), self._flat.size,
+                                                     C.byref(h)), "dsr_decoder_load")
+        self.handle = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                self.ctx.lib.dsr_decoder_free(self.ctx.handle, self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def decoder_from_state(state_dict, specs, device=None):
+    return Decoder(specs, fold_state(state_dict, specs), device)
+
+
+def config_decoder(experiment_directory, checkpoint="latest", device=None):
+    """workspace.py:202-223: specs.json + ModelParameters/<checkpoint>.pth -> decoder."""
+    import torch
+
+    specs = load_specs(experiment_directory)
+    if specs.get("NetworkArch", "deep_sdf_decoder") != "deep_sdf_decoder":
+        raise NotImplementedError("only NetworkArch=deep_sdf_decoder is supported")
+    saved = torch.load(os.path.join(experiment_directory, model_params_subdir, checkpoint + ".pth"),
+                       map_location="cpu", weights_only=True)
+    return decoder_from_state(saved["model_state_dict"], specs, device)

@@ -1,0 +1,177 @@
+"""ctypes binding of libdsr (include/dsr.h).
+
+The library is the product path: there is no Python/PyTorch fallback.  If
+``libdsr.so`` is missing or no gfx950 device is visible, every entry point
+raises ``DsrError`` ("Use ctypes.CDLL, which releases the GIL
+during a foreign call").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+DEFAULT_LIB = os.path.join(_PKG, "csrc", "libdsr.so")
+
+MAX_LAYERS = 16
+CODE_LEN = 64
+FAIL_REASONS = {0: "ok", 1: "sdf loss is NaN", 2: "fewer than 10 ray samples in the unit ball",
+                3: "render loss is NaN (no render points)"}
+
+
+class DsrError(RuntimeError):
+    pass
+
+
+FP = C.POINTER(C.c_float)
+IP = C.POINTER(C.c_int)
+
+
+class DecoderDesc(C.Structure):
+    _fields_ = [("code_len", C.c_int), ("n_layers", C.c_int),
+                ("out_dim", C.c_int * MAX_LAYERS), ("in_dim", C.c_int * MAX_LAYERS),
+                ("latent_in", C.c_int), ("use_tanh", C.c_int), ("xyz_in_all", C.c_int)]
+
+
+class OptimParams(C.Structure):
+    _fields_ = [("k1", C.c_float), ("k2", C.c_float), ("k3", C.c_float), ("k4", C.c_float),
+                ("b1", C.c_float), ("b2", C.c_float), ("lr", C.c_float), ("s_damp", C.c_float),
+                ("num_iterations", C.c_int), ("code_len", C.c_int),
+                ("num_depth_samples", C.c_int), ("cut_off", C.c_float),
+                ("pose_only_iterations", C.c_int)]
+
+
+class ObjectIn(C.Structure):
+    _fields_ = [("t_cam_obj", C.c_float * 16), ("pts", FP), ("n_pts", C.c_int),
+                ("rays", FP), ("n_rays", C.c_int), ("depth", FP), ("n_depth", C.c_int),
+                ("code", FP), ("pose_is_obj_cam", C.c_int)]
+
+
+class ObjectOut(C.Structure):
+    _fields_ = [("t_cam_obj", C.c_float * 16), ("code", C.c_float * CODE_LEN),
+                ("loss", C.c_float), ("is_good", C.c_int), ("fail_reason", C.c_int),
+                ("iters_done", C.c_int), ("n_valid_last", C.c_int), ("k_last", C.c_int)]
+
+
+class Trace(C.Structure):
+    _fields_ = [("H", FP), ("b", FP), ("dx", FP), ("loss", FP), ("sdf_loss", FP),
+                ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("fwd_ms", C.c_double), ("jac_ms", C.c_double), ("total_ms", C.c_double),
+                ("fwd_points", C.c_int64), ("jac_points", C.c_int64),
+                ("fwd_launches", C.c_int), ("jac_launches", C.c_int)]
+
+
+#: every function declared in include/dsr.h, with its ctypes signature
+SIGNATURES = {
+    "dsr_abi_version": (C.c_int, []),
+    "dsr_device_count": (C.c_int, [IP]),
+    "dsr_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "dsr_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "dsr_last_error": (C.c_char_p, [C.c_void_p]),
+    "dsr_decoder_load": (C.c_int, [C.c_void_p, C.POINTER(DecoderDesc), FP, C.c_size_t,
+                                   C.POINTER(C.c_void_p)]),
+    "dsr_decoder_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsr_reconstruct_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int,
+                                        C.POINTER(ObjectIn), C.POINTER(ObjectOut),
+                                        C.POINTER(Trace)]),
+    "dsr_batch_create": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int,
+                                   C.POINTER(ObjectIn), C.POINTER(C.c_void_p)]),
+    "dsr_batch_run": (C.c_int, [C.c_void_p]),
+    "dsr_batch_sync": (C.c_int, [C.c_void_p]),
+    "dsr_batch_download": (C.c_int, [C.c_void_p, C.POINTER(ObjectOut)]),
+    "dsr_batch_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "dsr_batch_destroy": (C.c_int, [C.c_void_p]),
+    "dsr_sdf_eval": (C.c_int, [C.c_void_p, C.c_void_p, FP, FP, C.c_int, FP, FP]),
+    "dsr_pose_only": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), FP, C.c_float,
+                                FP, C.c_int, FP, FP]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return os.environ.get("DSR_LIB", DEFAULT_LIB)
+
+
+def load_library(path: str | None = None):
+    """Load libdsr.so (once) and attach the ctypes signatures."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or lib_path()
+        if not os.path.isfile(p):
+            raise DsrError(f"libdsr not built: {p} is missing (run `make -C dsp-slam-rgbd_amd/csrc` "
+                           "or __graft_entry__.build()); there is no CPU fallback")
+        lib = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.dsr_abi_version() != 1:
+            raise DsrError("libdsr ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def fptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    return a.ctypes.data_as(FP)
+
+
+def iptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    return a.ctypes.data_as(IP)
+
+
+class Context:
+    """One libdsr context per HIP device (dsr_ctx_create)."""
+
+    _cache: dict[int, "Context"] = {}
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.dsr_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            msgs = {-3: "no HIP device visible", -4: "device is not gfx950 (MI355X)",
+                    -2: "bad device index", -1: "HIP runtime error"}
+            raise DsrError(f"dsr_ctx_create(device={device}) failed: {msgs.get(rc, rc)}")
+        self.handle = h
+        self.device = device
+
+    @classmethod
+    def get(cls, device: int | None = None) -> "Context":
+        if device is None:
+            device = int(os.environ.get("DSR_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        if device not in cls._cache:
+            cls._cache[device] = Context(device)
+        return cls._cache[device]
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.dsr_last_error(self.handle)
+            raise DsrError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def optim_params(cfg) -> OptimParams:
+    """configs.optimizer block (optimizer.py:27-43) -> OptimParams."""
+    jo = cfg["joint_optim"]
+    po = cfg.get("pose_only_optim", {"num_iterations": 5}) if hasattr(cfg, "get") else \
+        {"num_iterations": 5}
+    return OptimParams(float(jo["k1"]), float(jo["k2"]), float(jo["k3"]), float(jo["k4"]),
+                       float(jo["b1"]), float(jo["b2"]), float(jo["learning_rate"]),
+                       float(jo["scale_damping"]), int(jo["num_iterations"]), int(cfg["code_len"]),
+                       int(cfg["num_depth_samples"]), float(cfg["cut_off_threshold"]),
+                       int(po["num_iterations"]))

@@ -1,0 +1,177 @@
+/*
+ * dsr.h — C ABI of libdsr, the MI355X-native DeepSDF shape-prior reconstruction
+ * hot path (DSP-SLAM reconstruct/optimizer.py + loss.py + loss_utils.py +
+ * deep_sdf/deep_sdf_decoder.py).
+ *
+ * The reference exposes this path only as Python (`reconstruct.optimizer.Optimizer`,
+ * called from C++ ORB-SLAM2 through pybind11: src/LocalMapping_util.cc:181-182,
+ * :394-395, :109-110, src/MapObject_util.cc:43).  The build keeps that Python API
+ * (dsp-slam-rgbd_amd/reconstruct) and puts this library underneath it, loaded with
+ * ctypes.  Every entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *   - plain C types only; all matrices are row-major float32 (numpy C order);
+ *   - every function returns int status: 0 = ok, <0 = error (message via
+ *     dsr_last_error); numeric failure of an object is NOT an error — it is
+ *     reported per object in dsr_object_out.is_good (reference convention,
+ *     optimizer.py:132-152);
+ *   - the caller owns all host buffers for the duration of a call; the library
+ *     owns device memory; calls are synchronous unless stated otherwise;
+ *   - a context is bound to one HIP device and is not thread-safe (the reference's
+ *     callers are serialized on the GIL, include/System.h:57-71).
+ */
+#ifndef DSR_H
+#define DSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSR_ABI_VERSION 1
+#define DSR_MAX_LAYERS 16
+#define DSR_CODE_LEN 64
+
+typedef struct dsr_ctx dsr_ctx;
+typedef struct dsr_decoder dsr_decoder;
+typedef struct dsr_batch dsr_batch;
+
+/* Architecture of a DeepSDF decoder (replaces deep_sdf/deep_sdf_decoder.py:10-72 as
+ * configured by specs.json through deep_sdf/workspace.py:202-223).  Only the
+ * topology DSP-SLAM ships is implemented: weight-norm linear layers, latent
+ * re-injection at exactly one layer, ReLU, final self.th tanh; anything else is
+ * rejected with an error (never silently approximated). */
+typedef struct {
+  int code_len;                   /* CodeLength (64) */
+  int n_layers;                   /* number of lin{i} (9 for dims=[512]*8) */
+  int out_dim[DSR_MAX_LAYERS];    /* rows of lin{i}.weight */
+  int in_dim[DSR_MAX_LAYERS];     /* cols of lin{i}.weight */
+  int latent_in;                  /* index of the layer that takes cat([x, input]) (4) */
+  int use_tanh;                   /* NetworkSpecs.use_tanh — must be 0 */
+  int xyz_in_all;                 /* must be 0 */
+} dsr_decoder_desc;
+
+/* Optimizer hyper-parameters (reconstruct/optimizer.py:27-43; configs/config_*.json
+ * "optimizer" block). */
+typedef struct {
+  float k1, k2, k3, k4;           /* render, sdf, code-reg, rotation-prior weights */
+  float b1, b2;                   /* Huber thresholds render / sdf */
+  float lr;                       /* joint_optim.learning_rate */
+  float s_damp;                   /* joint_optim.scale_damping */
+  int num_iterations;             /* joint_optim.num_iterations */
+  int code_len;                   /* must equal the decoder's code_len */
+  int num_depth_samples;          /* M (50), <= 64 */
+  float cut_off;                  /* cut_off_threshold (0.01) */
+  int pose_only_iterations;       /* pose_only_optim.num_iterations (5) */
+} dsr_optim_params;
+
+/* One object handed to Optimizer.reconstruct_object(t_cam_obj, pts, rays, depth,
+ * code) — optimizer.py:90. */
+typedef struct {
+  float t_cam_obj[16];            /* initial object->camera Sim(3), row-major */
+  const float* pts;               /* (n_pts,3) surface points, camera frame */
+  int n_pts;
+  const float* rays;              /* (n_rays,3) ray directions, fg rays first */
+  int n_rays;
+  const float* depth;             /* (n_depth,) observed depth of the fg rays */
+  int n_depth;                    /* n_fg; n_rays - n_depth background rays */
+  const float* code;              /* (code_len,) warm-start code or NULL (=zeros) */
+  int pose_is_obj_cam;            /* 1: t_cam_obj[] already holds t_obj_cam (teacher forcing) */
+} dsr_object_in;
+
+enum {
+  DSR_OK = 0,
+  DSR_FAIL_SDF_NAN = 1,           /* optimizer.py:137-138 */
+  DSR_FAIL_RENDER_FEW = 2,        /* loss.py:86-88 -> optimizer.py:144-145 */
+  DSR_FAIL_RENDER_NAN = 3         /* optimizer.py:151-152 (includes K == 0) */
+};
+
+typedef struct {
+  float t_cam_obj[16];            /* optimized object->camera (valid iff is_good) */
+  float code[DSR_CODE_LEN];       /* optimized code (valid iff is_good) */
+  float loss;                     /* k1*render + k2*sdf of the last iteration, pre-update */
+  int is_good;
+  int fail_reason;                /* DSR_FAIL_* */
+  int iters_done;                 /* completed GN updates */
+  int n_valid_last, k_last;       /* ray samples in the unit ball / render points, last iter */
+} dsr_object_out;
+
+/* Optional per-iteration trace for tests (teacher-forced parity).  Arrays are
+ * [num_iterations] (H: [num_iterations][71*71]) for ONE object; the caller
+ * allocates. */
+typedef struct {
+  float* H;                       /* damped normal matrix that is inverted (optimizer.py:188) */
+  float* b;                       /* right-hand side */
+  float* dx;                      /* inv(H) b */
+  float* loss;                    /* k1*render+k2*sdf */
+  float* sdf_loss;
+  float* render_loss;
+  int* n_valid;
+  int* k;
+  float* t_obj_cam;               /* [num_iterations][16] state the iteration started from */
+  float* z;                       /* [num_iterations][code_len] */
+} dsr_trace;
+
+typedef struct {
+  double fwd_ms;                  /* summed device time of the ray-sample decoder kernel */
+  double jac_ms;                  /* summed device time of the fwd+Jacobian kernel */
+  double total_ms;                /* wall (device events) of the last run */
+  int64_t fwd_points;             /* sum over iterations/objects of N_valid */
+  int64_t jac_points;             /* sum of (N + K) */
+  int fwd_launches, jac_launches;
+} dsr_stats;
+
+/* ---- context ------------------------------------------------------------- */
+int dsr_abi_version(void);
+int dsr_ctx_create(int device, dsr_ctx** out);
+int dsr_ctx_destroy(dsr_ctx* ctx);
+const char* dsr_last_error(const dsr_ctx* ctx);
+int dsr_device_count(int* n);
+
+/* ---- decoder: replaces deep_sdf.workspace.config_decoder (workspace.py:202-223)
+ * + reconstruct.utils.get_decoder (utils.py:93-94).  `weights` holds the folded
+ * (weight-norm applied, W = g*v/||v||) layers back to back: for each layer i,
+ * W_i (out_dim x in_dim, row-major) then b_i (out_dim). */
+int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* desc, const float* weights,
+                     size_t n_floats, dsr_decoder** out);
+int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec);
+
+/* ---- joint shape + pose GN: replaces Optimizer.reconstruct_object
+ * (optimizer.py:90-205) for n_obj independent objects in one device pass.
+ * `trace` may be NULL; if not, it must point to n_obj dsr_trace records. */
+int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
+                          int n_obj, const dsr_object_in* in, dsr_object_out* out,
+                          const dsr_trace* trace);
+
+/* Resident batches for benchmarking / streaming (inputs uploaded once; a run
+ * re-initializes the optimizer state on device and executes all iterations on
+ * the context stream). */
+int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
+                     int n_obj, const dsr_object_in* in, dsr_batch** out);
+int dsr_batch_run(dsr_batch* b);                  /* async on the context stream */
+int dsr_batch_sync(dsr_batch* b);
+int dsr_batch_download(dsr_batch* b, dsr_object_out* out);
+int dsr_batch_stats(dsr_batch* b, dsr_stats* st);
+int dsr_batch_destroy(dsr_batch* b);
+
+/* ---- decoder queries: replaces decode_sdf / get_batch_sdf_jacobian
+ * (loss_utils.py:51-113) as used by Optimizer.compute_sdf_loss_objectpoint_zhjd
+ * (optimizer.py:207-213) and MeshExtractor.extract_mesh_from_code
+ * (optimizer.py:224-233).  pts are decoder-frame xyz; jac (n x (code_len+3)) may
+ * be NULL. */
+int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts,
+                 int n, float* sdf, float* jac);
+
+/* ---- pose-only SE(3) GN: replaces Optimizer.estimate_pose_cam_obj
+ * (optimizer.py:46-87).  t_co_se3: 4x4 SE(3) camera<-object, scale: object scale,
+ * result written to t_out (4x4). */
+int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
+                  const float* t_co_se3, float scale, const float* pts, int n_pts,
+                  const float* code, float* t_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSR_H */

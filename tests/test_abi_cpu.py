@@ -1,0 +1,95 @@
+"""The C ABI (include/dsr.h) without a GPU: the library loads, exports every declared
+entry point, its struct layouts match the ctypes mirror, and it fails loudly (no
+silent fallback) when no gfx950 device is present."""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import REPO
+
+HDR = os.path.join(REPO, "include", "dsr.h")
+
+
+def declared_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(dsr_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = declared_functions()
+    for f in ("dsr_ctx_create", "dsr_decoder_load", "dsr_reconstruct_batch", "dsr_sdf_eval",
+              "dsr_pose_only", "dsr_batch_run"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from reconstruct import _libdsr as L
+
+    lib = L.load_library()
+    fns = declared_functions()
+    assert set(fns) == set(L.SIGNATURES), set(fns) ^ set(L.SIGNATURES)
+    for f in fns:
+        assert hasattr(lib, f), f
+    out = subprocess.run(["nm", "-D", "--defined-only", L.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    for f in fns:
+        assert re.search(rf"\bT {f}$", out, flags=re.M), f
+    assert lib.dsr_abi_version() == 1
+
+
+STRUCTS = {"dsr_decoder_desc": "DecoderDesc", "dsr_optim_params": "OptimParams",
+           "dsr_object_in": "ObjectIn", "dsr_object_out": "ObjectOut", "dsr_trace": "Trace",
+           "dsr_stats": "Stats"}
+
+
+def test_struct_layouts_match_ctypes():
+    import ctypes
+
+    from reconstruct import _libdsr as L
+
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){"]
+    for cname, pyname in STRUCTS.items():
+        lines.append(f'printf("{pyname} size %zu\\n", sizeof({cname}));')
+        for fld, _ in getattr(L, pyname)._fields_:
+            lines.append(f'printf("{pyname} {fld} %zu\\n", offsetof({cname}, {fld}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "layout.c")
+        exe = os.path.join(d, "layout")
+        open(src, "w").write("\n".join(lines))
+        subprocess.run(["gcc", "-std=c99", "-o", exe, src], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    for line in out.strip().splitlines():
+        py, what, val = line.split()
+        cls = getattr(L, py)
+        if what == "size":
+            assert ctypes.sizeof(cls) == int(val), line
+        else:
+            assert getattr(cls, what).offset == int(val), line
+
+
+def test_no_device_fails_loudly():
+    """Without a visible gfx950 GPU, creating a context raises (no CPU fallback)."""
+    from reconstruct import _libdsr as L
+
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible")
+    except ImportError:
+        pass
+    with pytest.raises(L.DsrError):
+        L.Context(0)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from reconstruct import _libdsr as L
+
+    with pytest.raises(L.DsrError):
+        L.load_library(str(tmp_path / "nope.so"))

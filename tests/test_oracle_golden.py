@@ -1,0 +1,168 @@
+"""Pin the CPU oracle (oracle/dsr_oracle.py) to the reference's golden vectors.
+
+The fixtures were produced by the reference's own Python (tests/golden/make_golden.py,
+build container only).  These tests run on CPU and gate the oracle before it is
+trusted as the checker of the HIP path.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import synthetic as S
+from conftest import assert_jac_close, golden
+from oracle import dsr_oracle as O
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_fixture_decoder_is_the_generated_one(full_state):
+    g = golden("f0_fold.npz")
+    assert str(g["full_state_sha256"]) == S.state_sha256(full_state)
+
+
+def test_weight_norm_fold_bit_exact(full_layers):
+    """deep_sdf.workspace.fold_state (used by the product loader) == the reference
+    module's weight-norm hook, bit for bit (F0)."""
+    import hashlib
+
+    from deep_sdf.workspace import fold_state
+    from tests.golden.make_golden import SMALL_SPECS
+
+    g = golden("f0_fold.npz")
+    h = hashlib.sha256()
+    for W, b in full_layers:
+        h.update(W.tobytes())
+        h.update(b.tobytes())
+    assert h.hexdigest() == str(g["full_folded_sha256"])
+    import re
+
+    state = {}
+    for k in g.files:
+        m = re.match(r"state_module_lin(\d+)_(weight_g|weight_v|weight|bias)$", k)
+        if m:
+            state[f"module.lin{m.group(1)}.{m.group(2)}"] = g[k]
+    small = fold_state(state, SMALL_SPECS)
+    for i, (W, b) in enumerate(small):
+        assert np.array_equal(W, g[f"W{i}"]) and np.array_equal(b, g[f"b{i}"])
+
+
+@pytest.mark.parametrize("name", ["small", "full"])
+def test_decoder_fwd_jac(name):
+    from deep_sdf.workspace import fold_state
+    from tests.golden.make_golden import SMALL_SEED, SMALL_SPECS
+
+    g = golden(f"f1_decoder_{name}.npz")
+    if name == "small":
+        layers = fold_state(S.make_decoder(SMALL_SEED, SMALL_SPECS), SMALL_SPECS)
+        dec = O.Decoder(layers, 16, (4,))
+    else:
+        layers = fold_state(S.make_decoder(1234), S.DEFAULT_SPECS)
+        dec = O.Decoder(layers, 64, (4,))
+    L = g["z"].shape[0]
+    inp = np.concatenate([np.broadcast_to(g["z"], (g["x"].shape[0], L)), g["x"]], 1)
+    y, j = dec.forward_jac(inp)
+    assert np.abs(y - g["sdf"]).max() <= 2e-5
+    assert_jac_close(j, g["jac"])
+    assert np.abs(O.decode_sdf(dec, g["z"], g["x"]) - g["sdf_nograd"]).max() <= 2e-5
+
+
+def test_sdf_and_render_terms(oracle_dec):
+    """F2/F3: compute_sdf_loss / compute_render_loss at one state."""
+    f = golden("f23_terms.npz")
+    ob = S.redwood_object(0)
+    T, z = f["t_obj_cam"], f["z"]
+    jp, jc, r = O.compute_sdf_loss(oracle_dec, ob.pts, T, z)
+    assert np.abs(r - f["sdf_res"]).max() <= 2e-5
+    assert rel(jp, f["sdf_j_pose"]) <= 2e-5 and rel(jc, f["sdf_j_code"]) <= 2e-5
+    ren = O.compute_render_loss(oracle_dec, ob.rays, f["depth_obs"], T, f["depths"], z, 0.01)
+    # the sampled points are bit-exact (same fp32 op order as the reference)
+    assert np.array_equal(np.stack([ren.pts]), np.stack([f["render_pts"]]))
+    assert ren.n_valid == f["render_query"].shape[0]
+    assert ren.res.shape == f["render_res"].shape
+    assert np.abs(ren.res - f["render_res"]).max() <= 5e-5
+    assert rel(ren.j_pose, f["render_j_pose"]) <= 5e-4
+    assert rel(ren.j_code, f["render_j_code"]) <= 5e-4
+
+
+def test_linspace_and_small_math():
+    """F5: torch.linspace (fp32 CPU), exp_sim3 / exp_se3, Huber, rotation prior."""
+    f = golden("f5_math.npz")
+    for (a, b), ref in zip(f["linspace_ab"], f["linspace_out"]):
+        assert np.array_equal(O.linspace_torch(np.float32(a), np.float32(b), 50), ref)
+    for x, s3, se3 in zip(f["sim3_in"], f["sim3_out"], f["se3_out"]):
+        assert np.abs(O.exp_sim3(x) - s3).max() <= 2e-6
+        assert np.abs(O.exp_se3(x[:6]) - se3).max() <= 2e-6
+    rr, loss, w = O.get_robust_res(f["huber_res"].copy(), float(f["huber_b"]))
+    assert np.abs(rr - f["huber_rr"]).max() <= 1e-7
+    assert abs(loss - float(f["huber_loss"])) <= 1e-6 * float(f["huber_loss"])
+    for T, ref in zip(f["rot_t_obj_cam"], f["rot_out"]):
+        j, r = O.compute_rotation_loss_sim3(T)
+        assert abs(float(r) - ref[7]) <= 1e-6
+        assert np.abs(j - ref[:7]).max() <= 1e-5
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,optim", [("redwood0", S.REDWOOD_OPTIM), ("redwood1", S.REDWOOD_OPTIM)])
+def test_teacher_forced_iterations(oracle_dec, name, optim):
+    """F4: from every recorded reference state, one oracle GN step matches the reference's."""
+    f = golden(f"f4_traj_{name}.npz")
+    P = O.OptimParams.from_cfg(optim)
+    n_fg = f["obj_depth"].shape[0]
+    dobs = np.concatenate([f["obj_depth"], np.zeros(f["obj_rays"].shape[0] - n_fg)]).astype(np.float32)
+    jo = optim["joint_optim"]
+    for e in range(int(f["n_iters_run"])):
+        tr, _, _ = O.gn_step(oracle_dec, P, f["it_t_obj_cam"][e], f["it_z"][e], f["obj_pts"],
+                             f["obj_rays"], dobs, n_fg)
+        # depth samples: same formula; endpoints differ by <= 1 ulp (numpy vs torch 4x4 LU)
+        assert np.abs(O.linspace_torch(*_dminmax(f["it_t_obj_cam"][e]), 50)
+                      - f["it_depths"][e]).max() <= 4e-7 * np.abs(f["it_depths"][e]).max()
+        assert tr.n_valid == f["it_n_valid"][e]
+        assert abs(tr.k - f["it_k"][e]) <= 2
+        loss_ref = jo["k1"] * f["it_render_loss"][e] + jo["k2"] * f["it_sdf_loss"][e]
+        assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref)
+        assert rel(tr.H, f["it_H"][e]) <= 3e-3
+        assert rel(tr.b, f["it_b"][e]) <= 1e-2
+        assert rel(tr.dx, f["it_dx"][e]) <= 2e-2
+
+
+def _dminmax(t_obj_cam):
+    t_cam_obj = np.linalg.inv(t_obj_cam)
+    s = np.float32(np.linalg.det(t_cam_obj[:3, :3])) ** np.float32(1 / 3)
+    return t_cam_obj[2, 3] - s, t_cam_obj[2, 3] + s
+
+
+def test_reference_spread_fixture_is_consistent():
+    """The ensemble (other thread counts / 1-ulp pose perturbations) is recorded and
+    brackets a non-trivial spread: the noise floor for trajectory parity."""
+    for name in ("redwood0", "redwood1", "kitti0", "kitti5"):
+        f = golden(f"f4_traj_{name}.npz")
+        assert f["ens_loss"].shape[0] >= 4
+        assert np.isfinite(f["ens_loss"]).all()
+
+
+def test_failure_semantics():
+    """F6: the reference returns is_good=False, loss = previous (0. at iteration 0)."""
+    f = golden("f6_fail.npz")
+    assert not bool(f["few_is_good"]) and float(f["few_loss"]) == 0.0
+    assert int(f["few_iters"]) == 1
+
+
+def test_failure_few_points_oracle(oracle_dec):
+    f = golden("f6_fail.npz")
+    P = O.OptimParams.from_cfg(S.REDWOOD_OPTIM)
+    r = O.reconstruct_object(oracle_dec, P, f["few_t_cam_obj"], f["obj_pts"], f["obj_rays"],
+                             f["obj_depth"])
+    assert r.is_good == bool(f["few_is_good"]) and r.loss == float(f["few_loss"])
+
+
+def test_zhjd_and_pose_only(oracle_dec):
+    """F7: compute_sdf_loss_objectpoint_zhjd and estimate_pose_cam_obj."""
+    f = golden("f7_secondary.npz")
+    v = O.compute_sdf_loss_objectpoint(oracle_dec, f["zhjd_pts"], f["code"])
+    assert abs(float(v) - float(f["zhjd_out"])) <= 2e-6
+    P = O.OptimParams.from_cfg(S.KITTI_OPTIM)
+    T = O.estimate_pose_cam_obj(oracle_dec, P, f["t_se3"], float(f["scale"]), f["pts"], f["code"])
+    assert np.abs(T - f["pose_only_out"]).max() <= 1e-4 * np.abs(f["pose_only_out"]).max()
