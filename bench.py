@@ -96,6 +96,23 @@ def cpu_baseline(seconds_budget=30.0):
                       f"{P.num_iterations} GN iterations timed ({dt:.1f} s), extrapolated to 10"}
 
 
+def pmc_traffic():
+    """HBM bytes per k_mlp_fwd launch from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_summary.json, written by tools/prof_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes over this same default workload), or None."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json")), key=os.path.getmtime):
+        try:
+            d = json.load(open(f))
+            v = d["pmc"]["k_mlp_fwd"]["hbm_bytes_per_launch"]
+            best = (v, os.path.relpath(f, REPO))
+        except Exception:
+            continue
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,7 +224,7 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "k_mlp_fwd (decode_sdf on ray samples)",
                          "achieved": round(fwd_tf, 3), "peak": FP32_MFMA_PEAK_TF,
                          "unit": "TFLOP/s", "frac": round(fwd_tf / FP32_MFMA_PEAK_TF, 4),
-                         "traffic": None,
+                         "traffic": None, "traffic_unit": "bytes/launch (HBM+MALL, PMC)",
                          "flop_per_launch": fwd_flop / max(1, args.steps * 10),
                          "avg_launch_ms": fwd_ms / max(1, args.steps * 10)},
             "job_tflops": round(job_tf, 3),
@@ -215,6 +232,10 @@ def main():
             "good_fraction": n_good / float(n_obj * args.steps),
             "cpu_baseline": None,
         }
+        tr = pmc_traffic()
+        if tr is not None:
+            out["roofline"]["traffic"] = tr[0]
+            out["roofline"]["traffic_source"] = tr[1]
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

@@ -428,21 +428,26 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
         }
         occ[j] = ov;
       }
-      // cumprod of (1 - o) (loss.py:111), term probabilities, rendered depth (:112-125)
+      // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
+      // probabilities and rendered depth (:112-125).  The 51-term sum is accumulated in
+      // fp64 and rounded once: torch's vectorised fp32 sum is within ~1 ulp of exact,
+      // a sequential fp32 sum is not (d ~ 15 m, residual d_obs - d_u ~ 1 cm).
       float T = 1.f;
+      double dud = 0.0;
       for (int j = 0; j < M; ++j) {
         const float tp = occ[j] * T;
         T = T * (1.f - occ[j]);
         Tr[j] = T;
-        du = du + S.depths[j] * tp;
+        dud += (double)(S.depths[j] * tp);
       }
-      du = du + (1.1f * dmax) * T;                   // background bin o=1, d=1.1*d_max
+      dud += (double)((1.1f * dmax) * T);            // background bin o=1, d=1.1*d_max
+      du = (float)dud;
       dob = dobs_all[d.ray_off + ray];
       for (uint64_t m = grad; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
-        float sacc = 0.f;
-        for (int l = j; l < M; ++l) sacc = sacc + Tr[l];
-        const float dedo = sacc / (1.f - occ[j]);     // :131-132
+        double sacc = 0.0;
+        for (int l = j; l < M; ++l) sacc += (double)Tr[l];
+        const float dedo = (float)sacc / (1.f - occ[j]);     // :131-132
         if (dedo > 1e-2f) ++cnt;                      // :135
       }
     }
@@ -456,9 +461,9 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
       res = res < -0.30f ? -0.30f : res;
       for (uint64_t m = grad; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
-        float sacc = 0.f;
-        for (int l = j; l < M; ++l) sacc = sacc + Tr[l];
-        const float dedo = sacc / (1.f - occ[j]);
+        double sacc = 0.0;
+        for (int l = j; l < M; ++l) sacc += (double)Tr[l];
+        const float dedo = (float)sacc / (1.f - occ[j]);
         if (dedo > 1e-2f) {
           const float deds = (dedo * delta_d) * do_ds;  // :142
           const float3 x = ray_sample(rays, S, ray, j);
@@ -704,12 +709,12 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ int piv[NPAR];
   __shared__ int flag;
   const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
-  for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {
-    float a = 0.f, b = 0.f;
-    for (int t = 0; t < ns; ++t) a += slots[(size_t)(d.slot_sdf + t) * SLOT_FLOATS + e];
-    for (int t = 0; t < nk; ++t) b += slots[(size_t)(d.slot_sdf + ns + t) * SLOT_FLOATS + e];
-    Ss[e] = a;
-    Sr[e] = b;
+  for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {   // tile partials, fp64 combine
+    double a = 0.0, b = 0.0;
+    for (int t = 0; t < ns; ++t) a += (double)slots[(size_t)(d.slot_sdf + t) * SLOT_FLOATS + e];
+    for (int t = 0; t < nk; ++t) b += (double)slots[(size_t)(d.slot_sdf + ns + t) * SLOT_FLOATS + e];
+    Ss[e] = (float)a;
+    Sr[e] = (float)b;
   }
   if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
   __syncthreads();

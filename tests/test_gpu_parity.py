@@ -34,6 +34,15 @@ def rel(a, b):
     return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def step_err(dx, dx_ref, H):
+    """GN step error in the H-norm, sqrt(d'Hd / dx'H dx): insensitive to the badly
+    determined directions (e.g. yaw of a near-rotationally-symmetric shape) where the
+    quadratic model is flat and tiny b differences move dx a lot at no cost."""
+    d = np.asarray(dx, np.float64) - dx_ref
+    H = np.asarray(H, np.float64)
+    return float(np.sqrt(max(d @ H @ d, 0.0) / max(dx_ref @ H @ dx_ref, 1e-300)))
+
+
 def test_library_is_native(gpu_decoder):
     from reconstruct import _libdsr as L
 
@@ -93,10 +102,18 @@ def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
         assert abs(int(t["n_valid"][0]) - int(f["it_n_valid"][e])) <= 2
         assert abs(int(t["k"][0]) - int(f["it_k"][e])) <= 2
         loss_ref = jo["k1"] * f["it_render_loss"][e] + jo["k2"] * f["it_sdf_loss"][e]
-        assert abs(t["loss"][0] - loss_ref) <= 1e-5 * abs(loss_ref)
+        # identical render set -> 1e-5; each flipped render point moves the mean Huber
+        # loss by at most (2 b1 0.3 - b1^2)/K <= 0.09/K (clamp +-0.30, loss.py:147-148)
+        dk = abs(int(t["k"][0]) - int(f["it_k"][e]))
+        tol = 1e-5 * abs(loss_ref) + dk * jo["k1"] * 0.09 / f["it_k"][e]
+        assert abs(t["loss"][0] - loss_ref) <= tol, (e, dk)
+        if dk == 0:
+            assert abs(t["render_loss"][0] - f["it_render_loss"][e]) <= 1e-5 * f["it_render_loss"][e]
+            assert abs(t["sdf_loss"][0] - f["it_sdf_loss"][e]) <= 1e-5 * f["it_sdf_loss"][e]
         assert rel(t["H"][0], f["it_H"][e]) <= 2e-3, e
         assert rel(t["b"][0], f["it_b"][e]) <= 1e-2, e
-        assert rel(t["dx"][0], f["it_dx"][e]) <= 1e-2, e
+        assert step_err(t["dx"][0], f["it_dx"][e], f["it_H"][e]) <= 1e-2, e
+        assert rel(t["dx"][0], f["it_dx"][e]) <= 5e-2, e
 
 
 @pytest.mark.parametrize("name,optim,dtype", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),
@@ -138,7 +155,7 @@ def test_trajectory_shadowing_and_final(gpu_decoder, oracle_dec, name, optim, dt
         assert abs(int(tg["n_valid"][0]) - tro.n_valid) <= 2
         assert abs(tg["loss"][0] - tro.loss) <= 1e-4 * abs(tro.loss)
         assert rel(tg["H"][0], tro.H) <= 5e-3
-        assert rel(tg["dx"][0], tro.dx) <= 2e-2
+        assert step_err(tg["dx"][0], tro.dx, tro.H) <= 2e-2
     assert np.isfinite(t["loss"]).all()
 
 
