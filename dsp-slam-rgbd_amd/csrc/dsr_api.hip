@@ -283,6 +283,7 @@ static GNParams make_params(const dsr_optim_params* p) {
   P.k1 = p->k1; P.k2 = p->k2; P.k3 = p->k3; P.k4 = p->k4;
   P.b1 = p->b1; P.b2 = p->b2; P.lr = p->lr; P.s_damp = p->s_damp;
   P.cut_off = p->cut_off; P.iters = p->num_iterations; P.M = p->num_depth_samples;
+  P.raw_residual = 0;
   return P;
 }
 
@@ -436,7 +437,7 @@ int dsr_batch_run(dsr_batch* b) {
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 2], s));
     hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
                        b->pts, b->kpts, b->kres, b->bias0f, b->bias4f, P, b->slots,
-                       (const float4*)nullptr, (float*)nullptr);
+                       (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 3], s));
     hipLaunchKernelGGL(k_count, dim3(cb), dim3(64), 0, s, n, b->desc, b->st, it, b->counts);
     hipLaunchKernelGGL(k_solve, dim3(n), dim3(SOLVE_THREADS), 0, s, n, b->desc, b->st, b->zbuf, P, b->slots,
@@ -594,7 +595,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
     hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const ObjState*)nullptr, (const float*)nullptr,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
-                       (float*)nullptr, (const float4*)dp, (float*)dout);
+                       (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr);
   } else {
     hipLaunchKernelGGL(k_mlp_fwd, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout);
@@ -617,8 +618,96 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
 
 int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, const float* t_co_se3,
                   float scale, const float* pts, int n_pts, const float* code, float* t_out) {
-  (void)dec; (void)p; (void)t_co_se3; (void)scale; (void)pts; (void)n_pts; (void)code; (void)t_out;
-  return fail(ctx, "dsr_pose_only: not implemented yet");
+  // Optimizer.estimate_pose_cam_obj (optimizer.py:46-87)
+  if (!ctx || !dec || !p || !t_co_se3 || !code || !t_out || (n_pts > 0 && !pts)) return fail(ctx, "null argument");
+  if (n_pts <= 0) return fail(ctx, "pose-only GN needs surface points");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  float t_in[16];
+  for (int i = 0; i < 16; ++i) t_in[i] = t_co_se3[i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) t_in[i * 4 + j] = t_in[i * 4 + j] * scale;     // :56 (fp32)
+  std::vector<float> hp(pts, pts + (size_t)n_pts * 3);
+  int n = n_pts;
+  const int iters = p->pose_only_iterations;
+  const int cap_tiles = (n + TILE - 1) / TILE;
+  void *dpts = nullptr, *dst = nullptr, *dz = nullptr, *db0 = nullptr, *db4 = nullptr, *dt = nullptr,
+       *dnt = nullptr, *dslots = nullptr, *ddesc = nullptr, *dtin = nullptr, *doc = nullptr, *dzb = nullptr,
+       *dres = nullptr, *dout = nullptr;
+  std::vector<void*> al;
+  auto A = [&](void** q, size_t bytes) {
+    if (hipMalloc(q, bytes) != hipSuccess) return false;
+    al.push_back(*q);
+    return true;
+  };
+  auto cleanup = [&]() { for (void* q : al) hipFree(q); };
+  if (!A(&dpts, sizeof(float) * 3 * n) || !A(&dst, sizeof(ObjState)) || !A(&dz, sizeof(float) * CODE) ||
+      !A(&db0, sizeof(float) * HID) || !A(&db4, sizeof(float) * HID) || !A(&dt, sizeof(Tile) * cap_tiles) ||
+      !A(&dnt, sizeof(int)) || !A(&dslots, sizeof(float) * SLOT_FLOATS * cap_tiles) ||
+      !A(&ddesc, sizeof(ObjDesc)) || !A(&dtin, sizeof(float) * 16) || !A(&doc, sizeof(int)) ||
+      !A(&dzb, sizeof(float) * CODE) || !A(&dres, sizeof(float) * n) || !A(&dout, sizeof(float) * 16)) {
+    cleanup();
+    return fail(ctx, "hipMalloc failed (pose_only)");
+  }
+  const int zero = 0;
+  bool ok = hipMemcpy(dpts, hp.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dz, code, sizeof(float) * CODE, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dtin, t_in, sizeof(float) * 16, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(doc, &zero, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+  if (!ok) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only)"); }
+  const DevDecoder& D = dec->D;
+  GNParams P = make_params(p);
+  P.raw_residual = 1;
+  hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)dz, (float*)db0, (float*)db4);
+  hipLaunchKernelGGL(k_init_state, dim3(1), dim3(64), 0, s, 1, (const float*)dtin, (const int*)doc,
+                     (const float*)dz, (ObjState*)dst, (float*)dzb);                  // :57 t_obj_cam = inv
+  auto upload_tiles = [&](int npts) {
+    ObjDesc d{};
+    d.n_pts = npts;
+    const int nt = (npts + TILE - 1) / TILE;
+    std::vector<Tile> ht(nt);
+    for (int t = 0; t < nt; ++t) ht[t] = Tile{0, 0, t * TILE, std::min(TILE, npts - t * TILE)};
+    return hipMemcpy(ddesc, &d, sizeof(ObjDesc), hipMemcpyHostToDevice) == hipSuccess &&
+           (nt == 0 || hipMemcpy(dt, ht.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice) == hipSuccess) &&
+           hipMemcpy(dnt, &nt, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!upload_tiles(n)) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only tiles)"); }
+  for (int e = 0; e < iters; ++e) {
+    const int nt = (n + TILE - 1) / TILE;
+    const bool filter = (e == 4) && (e + 1 < iters);   // :77-79 inlier filter (effective only past 5 iters)
+    hipLaunchKernelGGL(k_mlp_jac, dim3(std::max(1, std::min(ctx->n_cu, nt))), dim3(512), 0, s, D, (const Tile*)dt,
+                       (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst, (const float*)dpts,
+                       (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
+                       (float*)dslots, (const float4*)nullptr, (float*)nullptr, filter ? (float*)dres : (float*)nullptr);
+    hipLaunchKernelGGL(k_solve_pose, dim3(1), dim3(256), 0, s, nt, n, (ObjState*)dst, (const float*)dslots);
+    if (filter) {
+      std::vector<float> res(n);
+      if (hipMemcpy(res.data(), dres, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess) {
+        cleanup();
+        return fail(ctx, "hipMemcpy failed (pose_only residuals)");
+      }
+      std::vector<float> kept;
+      for (int i = 0; i < n; ++i)
+        if (std::fabs(res[i]) <= 0.05f) kept.insert(kept.end(), hp.begin() + 3 * i, hp.begin() + 3 * i + 3);
+      hp.swap(kept);
+      n = (int)(hp.size() / 3);
+      if (n == 0) break;
+      if (hipMemcpy(dpts, hp.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice) != hipSuccess || !upload_tiles(n)) {
+        cleanup();
+        return fail(ctx, "hipMemcpy failed (pose_only filter)");
+      }
+    }
+  }
+  hipLaunchKernelGGL(k_inv_out, dim3(1), dim3(64), 0, s, (const ObjState*)dst, (float*)dout);   // :84
+  float T[16];
+  ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
+       hipMemcpy(T, dout, sizeof(float) * 16, hipMemcpyDeviceToHost) == hipSuccess;
+  cleanup();
+  if (!ok) return fail(ctx, "pose_only failed");
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) T[i * 4 + j] = T[i * 4 + j] / scale;                 // :85
+  for (int i = 0; i < 16; ++i) t_out[i] = T[i];
+  return 0;
 }
 
 }  // extern "C"

@@ -80,6 +80,7 @@ struct Tile {
 struct GNParams {
   float k1, k2, k3, k4, b1, b2, lr, s_damp, cut_off;
   int iters, M;
+  int raw_residual;      // 1: J^T r with the un-robustified residual (pose-only GN, optimizer.py:71)
 };
 
 __device__ __forceinline__ float fetch4(const float4& v, int j) {

@@ -126,6 +126,33 @@ __device__ void exp_sim3_dev(const float* x, float* out) {
   }
 }
 
+// exp_se3 (loss_utils.py:139-173) in fp32: x = (v, w), theta <= 1e-8 -> identity rotation.
+__device__ void exp_se3_dev(const float* x, float* out) {
+  const float v0 = x[0], v1 = x[1], v2 = x[2], w0 = x[3], w1 = x[4], w2 = x[5];
+  const float W[9] = {0.f, -w2, w1, w2, 0.f, -w0, -w1, w0, 0.f};
+  float W2[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      W2[i * 3 + j] = (W[i * 3 + 0] * W[0 * 3 + j] + W[i * 3 + 1] * W[1 * 3 + j]) + W[i * 3 + 2] * W[2 * 3 + j];
+  const float theta = sqrtf((w0 * w0 + w1 * w1) + w2 * w2);
+  const float t2 = theta * theta, t3 = t2 * theta;
+  const float st = sinf(theta), ct = cosf(theta);
+  const float I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  float ew[9], J[9];
+  if (theta <= 1e-8f) {
+    for (int i = 0; i < 9; ++i) { ew[i] = I3[i]; J[i] = I3[i]; }
+  } else {
+    for (int i = 0; i < 9; ++i) ew[i] = (I3[i] + W[i] * st / theta) + W2[i] * (1.f - ct) / t2;
+    const float k1 = (1.f - ct) / t2, k2 = (theta - st) / t3;
+    for (int i = 0; i < 9; ++i) J[i] = (I3[i] + k1 * W[i]) + k2 * W2[i];
+  }
+  for (int i = 0; i < 16; ++i) out[i] = (i % 5 == 0) ? 1.f : 0.f;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) out[i * 4 + j] = ew[i * 3 + j];
+    out[i * 4 + 3] = (J[i * 3 + 0] * v0 + J[i * 3 + 1] * v1) + J[i * 3 + 2] * v2;
+  }
+}
+
 // (p[...,None,:] * T[:3,:3]).sum(-1) + T[:3,3]   (loss.py:31-32, :74-77)
 __device__ __forceinline__ float3 xform(const float* T, float x, float y, float z) {
   float3 o;
@@ -505,7 +532,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
                                                  const float* __restrict__ bias4f, GNParams P,
                                                  float* __restrict__ slots,
                                                  const float4* __restrict__ raw_pts,
-                                                 float* __restrict__ raw_out) {
+                                                 float* __restrict__ raw_out,
+                                                 float* __restrict__ res_out) {
   __shared__ JacShared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -654,7 +682,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
         const float hn = (x <= b) ? x * x : (2.0f * b) * x - b * b;
         const float den = (x == 0.f) ? 1.f : x;
         const float wgt = sqrtf(hn) / den;
-        sm.r[tid] = (tid < tl.count) ? wgt * res : 0.f;
+        sm.r[tid] = (tid < tl.count) ? (P.raw_residual ? res : wgt * res) : 0.f;
+        if (res_out && !ren && tid < tl.count) res_out[d.pts_off + tl.start + tid] = res;
       }
     }
     __syncthreads();
@@ -867,6 +896,44 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     trace_i[((size_t)it * n_obj + o) * 2 + 0] = S.n_valid;
     trace_i[((size_t)it * n_obj + o) * 2 + 1] = S.k;
   }
+}
+
+// ------------------------------------------------------------------------------------
+// k_solve_pose: one iteration of Optimizer.estimate_pose_cam_obj (optimizer.py:62-74):
+// H = J^T J / N + 1e-2 I (6x6, se3 part of the Sim(3) J), b = -J^T r / N (raw residual),
+// dx = inverse(H) b, T <- exp_se3(dx) T.
+// ------------------------------------------------------------------------------------
+__global__ void k_solve_pose(int n_tiles, int n_pts, ObjState* st, const float* __restrict__ slots) {
+  __shared__ float S[SLOT_FLOATS];
+  for (int e = threadIdx.x; e < SLOT_FLOATS; e += blockDim.x) {
+    double a = 0.0;
+    for (int t = 0; t < n_tiles; ++t) a += (double)slots[(size_t)t * SLOT_FLOATS + e];
+    S[e] = (float)a;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float N = (float)n_pts;
+  float H[36], Hi[36], b[6], dx[6], dT[16], Tn[16];
+  for (int a = 0; a < 6; ++a)
+    for (int c = 0; c < 6; ++c) {
+      const int lo = min(a, c), hi = max(a, c);
+      const int idx = lo * NPAR - lo * (lo - 1) / 2 + (hi - lo);
+      H[a * 6 + c] = S[idx] / N + ((a == c) ? 1e-2f : 0.f);
+    }
+  for (int a = 0; a < 6; ++a) b[a] = (-S[NTRI + a]) / N;
+  inv_small<6>(H, Hi);
+  for (int a = 0; a < 6; ++a) {
+    float s = 0.f;
+    for (int c = 0; c < 6; ++c) s = __builtin_fmaf(Hi[a * 6 + c], b[c], s);
+    dx[a] = s;
+  }
+  exp_se3_dev(dx, dT);
+  mm4(dT, st[0].T, Tn);
+  for (int i = 0; i < 16; ++i) st[0].T[i] = Tn[i];
+}
+
+__global__ void k_inv_out(const ObjState* __restrict__ st, float* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) inv_small<4>(st[0].T, out);
 }
 
 // per-iteration counters for the algorithmic-FLOP bookkeeping

@@ -111,7 +111,9 @@ def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
             assert abs(t["render_loss"][0] - f["it_render_loss"][e]) <= 1e-5 * f["it_render_loss"][e]
             assert abs(t["sdf_loss"][0] - f["it_sdf_loss"][e]) <= 1e-5 * f["it_sdf_loss"][e]
         assert rel(t["H"][0], f["it_H"][e]) <= 2e-3, e
-        assert rel(t["b"][0], f["it_b"][e]) <= 1e-2, e
+        # b[3:6] carries k4 * J_rot * r_rot with k4 = 1e7 and r_rot = 1 - cos(tilt), an fp32
+        # cancellation in the reference itself: max-norm loose, step in the H-norm tight
+        assert rel(t["b"][0], f["it_b"][e]) <= 5e-2, e
         assert step_err(t["dx"][0], f["it_dx"][e], f["it_H"][e]) <= 1e-2, e
         assert rel(t["dx"][0], f["it_dx"][e]) <= 5e-2, e
 
@@ -219,3 +221,96 @@ def test_full_size_batch_properties(gpu_decoder):
     for r in res:
         assert np.isfinite(r["t_cam_obj"]).all() and np.isfinite(r["code"]).all()
         assert np.isfinite(r["loss"]) and r["loss"] > 0
+
+
+def test_pose_only_vs_golden(gpu_decoder, oracle_dec):
+    """estimate_pose_cam_obj (optimizer.py:46-87) on device vs the reference (F7) and the oracle."""
+    from oracle import dsr_oracle as O
+
+    f = golden("f7_secondary.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, "KITTI")
+    T = opt.estimate_pose_cam_obj(f["t_se3"], float(f["scale"]), f["pts"], f["code"])
+    ref = f["pose_only_out"]
+    assert T.dtype == np.float32 and T.shape == (4, 4)
+    assert np.abs(T - ref).max() <= 2e-5 * np.abs(ref).max(), np.abs(T - ref).max()
+    To = O.estimate_pose_cam_obj(oracle_dec, O.OptimParams.from_cfg(S.KITTI_OPTIM), f["t_se3"],
+                                 float(f["scale"]), f["pts"], f["code"])
+    assert np.abs(T - To).max() <= 2e-5 * np.abs(To).max()
+
+
+def test_pose_only_more_iterations_filters_inliers(gpu_decoder, oracle_dec):
+    """With >5 pose-only iterations the e==4 inlier filter (optimizer.py:77-79) takes effect."""
+    from oracle import dsr_oracle as O
+
+    cfg = dict(S.KITTI_OPTIM, pose_only_optim={"num_iterations": 7, "learning_rate": 1.0})
+    opt = _opt(gpu_decoder, cfg, "KITTI")
+    ob = S.kitti_object(11)
+    T0 = ob.t_cam_obj.copy()
+    s = float(np.cbrt(np.linalg.det(T0[:3, :3].astype(np.float64))))
+    T0[:3, :3] /= s
+    # a code of norm ~4 makes the shape visibly non-spherical, so yaw is observable and the
+    # comparison is not dominated by the 1e-2 damping of an unobservable direction
+    code = (0.5 * np.random.default_rng(3).standard_normal(64)).astype(np.float32)
+    T = opt.estimate_pose_cam_obj(T0, s, ob.pts[:700], code)
+    P = O.OptimParams.from_cfg(cfg)
+    To = O.estimate_pose_cam_obj(oracle_dec, P, T0, s, ob.pts[:700], code)
+    assert np.abs(T - To).max() <= 2e-4 * np.abs(To).max()
+
+
+def _gpu_shard_worker(rank, world, port, q):
+    import os
+    import sys
+
+    from conftest import PKG, REPO
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DSR_DEVICE="0")
+    import torch.distributed as dist
+
+    import synthetic as S
+    from conftest import make_cfg
+    from deep_sdf.workspace import decoder_from_state
+    from reconstruct.optimizer import Optimizer
+    from reconstruct.parallel import reconstruct_sharded
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS, device=0)
+        opt = Optimizer(dec, make_cfg(S.REDWOOD_OPTIM, "Redwood"))
+        objs = [(o.t_cam_obj, o.pts, o.rays, o.depth, None)
+                for o in (S.redwood_object(i, n_pts=300) for i in range(6))]
+        res = reconstruct_sharded(objs, opt.reconstruct_objects)
+        if rank == 0:
+            q.put([(r["is_good"], r["loss"], r["t_cam_obj"].tolist()) for r in res])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_on_device(gpu_decoder):
+    """reconstruct_sharded with the real device solver (2 ranks sharing GPU 0, gloo for the
+    gather here; RCCL on a multi-GPU node) == one batched call, bitwise."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")
+    ref = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None)
+                                   for o in (S.redwood_object(i, n_pts=300) for i in range(6))])
+    for (good, loss, T), r in zip(got, ref):
+        assert good and r["is_good"]
+        assert np.float32(loss) == np.float32(r["loss"])
+        assert np.array_equal(np.asarray(T, np.float32), r["t_cam_obj"])
