@@ -15,14 +15,37 @@
 #include "../../include/dsr.h"
 #include "dsr_kernels.hpp"
 
+#ifndef DSR_DEFAULT_FWD_VARIANT
+#define DSR_DEFAULT_FWD_VARIANT 6   // B prefetch + s_setprio (A/B: tools/fwd_variants.py)
+#endif
+
 using namespace dsr;
 
 struct dsr_ctx {
   int device = 0;
   int n_cu = 256;
   hipStream_t stream = nullptr;
+  unsigned* sync_ctr = nullptr;    // 8 groups x 32 uints (128-B apart) for the fwd soft sync
   std::string err;
 };
+
+// Forward-kernel variant (DSR_FWD_VARIANT, bit0 XCD soft sync, bit1 B prefetch, bit2 setprio)
+using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
+                           const float*, float*, unsigned*);
+static FwdKernel fwd_kernel(int v) {
+  switch (v & 7) {
+    case 1: return k_mlp_fwd<1>;
+    case 2: return k_mlp_fwd<2>;
+    case 3: return k_mlp_fwd<3>;
+    case 6: return k_mlp_fwd<6>;
+    case 7: return k_mlp_fwd<7>;
+    default: return k_mlp_fwd<0>;
+  }
+}
+static int fwd_variant() {
+  const char* e = getenv("DSR_FWD_VARIANT");
+  return e ? atoi(e) : DSR_DEFAULT_FWD_VARIANT;
+}
 
 struct dsr_decoder {
   dsr_ctx* ctx = nullptr;
@@ -107,6 +130,11 @@ int dsr_ctx_create(int device, dsr_ctx** out) {
     delete c;
     return -1;
   }
+  if (hipMalloc(&c->sync_ctr, 8 * 32 * sizeof(unsigned)) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return -1;
+  }
   *out = c;
   return 0;
 }
@@ -115,6 +143,7 @@ int dsr_ctx_destroy(dsr_ctx* ctx) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  if (ctx->sync_ctr) hipFree(ctx->sync_ctr);
   delete ctx;
   return 0;
 }
@@ -419,6 +448,7 @@ int dsr_batch_run(dsr_batch* b) {
   const GNParams P = b->P;
   const int grid = ctx->n_cu;
   const int cb = (n + 63) / 64;
+  const FwdKernel fwdk = fwd_kernel(fwd_variant());
   DSR_CHECK(ctx, hipEventRecord(b->ev[0], s));
   hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
   for (int it = 0; it < b->iters; ++it) {
@@ -427,9 +457,10 @@ int dsr_batch_run(dsr_batch* b) {
     hipLaunchKernelGGL(k_sample, dim3(n), dim3(SAMPLE_THREADS), 0, s, n, b->desc, b->st, b->rays, b->M,
                        b->cand, b->dense);
     hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_f, b->nt_f);
+    DSR_CHECK(ctx, hipMemsetAsync(ctx->sync_ctr, 0, 8 * 32 * sizeof(unsigned), s));
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 0], s));
-    hipLaunchKernelGGL(k_mlp_fwd, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
-                       b->bias0f, b->bias4f, b->dense);
+    hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
+                       b->bias0f, b->bias4f, b->dense, ctx->sync_ctr);
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 1], s));
     hipLaunchKernelGGL(k_render, dim3(n), dim3(RENDER_THREADS), 0, s, n, b->desc, b->st, b->rays, b->dobs, P,
                        b->dense, b->kpts, b->kres);
@@ -597,8 +628,9 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
                        (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr);
   } else {
-    hipLaunchKernelGGL(k_mlp_fwd, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
-                       (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout);
+    hipLaunchKernelGGL(k_mlp_fwd<0>, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+                       (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
+                       (unsigned*)nullptr);
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     cleanup();
@@ -682,7 +714,8 @@ int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* 
     hipLaunchKernelGGL(k_solve_pose, dim3(1), dim3(256), 0, s, nt, n, (ObjState*)dst, (const float*)dslots);
     if (filter) {
       std::vector<float> res(n);
-      if (hipMemcpy(res.data(), dres, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess) {
+      if (hipStreamSynchronize(s) != hipSuccess ||      // ctx->stream is non-blocking
+          hipMemcpy(res.data(), dres, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess) {
         cleanup();
         return fail(ctx, "hipMemcpy failed (pose_only residuals)");
       }
@@ -691,7 +724,12 @@ int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* 
         if (std::fabs(res[i]) <= 0.05f) kept.insert(kept.end(), hp.begin() + 3 * i, hp.begin() + 3 * i + 3);
       hp.swap(kept);
       n = (int)(hp.size() / 3);
-      if (n == 0) break;
+      if (n == 0) {
+        // the reference goes on with an empty point set: J^T J / 0 -> NaN pose
+        for (int i = 0; i < 16; ++i) t_out[i] = __builtin_nanf("");
+        cleanup();
+        return 0;
+      }
       if (hipMemcpy(dpts, hp.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice) != hipSuccess || !upload_tiles(n)) {
         cleanup();
         return fail(ctx, "hipMemcpy failed (pose_only filter)");

@@ -359,18 +359,33 @@ struct FwdShared {
   float red[NWAVE * TILE];
 };
 
+// V bit0: per-tile soft sync of each XCD's workgroups (L2 reuse of the layer weights)
+// V bit1: B-fragment prefetch GEMM; V bit2: s_setprio around MFMA clusters
+template <int V>
+__device__ __forceinline__ void fwd_gemm(const float4* A, int T, const float* Hs, floatx4 (&acc)[4][4],
+                                         int lane) {
+  if constexpr ((V & 2) != 0) gemm_tile_pf<4, (V & 4) != 0>(A, T, Hs, acc, lane);
+  else gemm_tile<4>(A, T, Hs, acc, lane);
+}
+
+template <int V>
 __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __restrict__ tiles,
                                                  const int* __restrict__ n_tiles,
                                                  const ObjDesc* __restrict__ desc,
                                                  const float4* __restrict__ cand,
                                                  const float* __restrict__ bias0f,
                                                  const float* __restrict__ bias4f,
-                                                 float* __restrict__ dense) {
+                                                 float* __restrict__ dense,
+                                                 unsigned* __restrict__ sync_ctr) {
   __shared__ FwdShared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = *n_tiles;
-  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+  const int rounds = (nt + gridDim.x - 1) / gridDim.x;
+  for (int r = 0; r < rounds; ++r) {
+    const int ti = blockIdx.x + r * gridDim.x;
+    if constexpr ((V & 1) != 0) group_soft_sync(sync_ctr, r);
+    if (ti >= nt) continue;
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
     const float4* src = cand + d.cand_off + tl.start;
@@ -386,14 +401,14 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
     floatx4 acc[4][4];
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 16;
-      gemm_tile<4>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      fwd_gemm<V>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
       epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mask, l == 3);
       __syncthreads();
     }
     {
       const int T = D.Kf[7] / 16;
-      gemm_tile<4>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      fwd_gemm<V>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       epi_l7(acc, D, sm.red, w, lane, mask);
     }
     __syncthreads();
@@ -521,6 +536,16 @@ struct JacShared {
 
 constexpr int JPITCH = 72;
 
+#ifndef DSR_JAC_VARIANT
+#define DSR_JAC_VARIANT 6
+#endif
+template <int V>
+__device__ __forceinline__ void jac_gemm(const float4* A, int T, const float* Hs, floatx4 (&acc)[4][4],
+                                         int lane) {
+  if constexpr ((V & 2) != 0) gemm_tile_pf<4, (V & 4) != 0>(A, T, Hs, acc, lane);
+  else gemm_tile<4>(A, T, Hs, acc, lane);
+}
+
 __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __restrict__ tiles,
                                                  const int* __restrict__ n_tiles,
                                                  const ObjDesc* __restrict__ desc,
@@ -535,6 +560,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
                                                  float* __restrict__ raw_out,
                                                  float* __restrict__ res_out) {
   __shared__ JacShared sm;
+  constexpr int JV = DSR_JAC_VARIANT;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = *n_tiles;
@@ -571,14 +597,14 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
 #pragma unroll
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 16;
-      gemm_tile<4>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      jac_gemm<JV>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
       epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mk[l], l == 3);
       __syncthreads();
     }
     {
       const int T = D.Kf[7] / 16;
-      gemm_tile<4>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      jac_gemm<JV>(D.Wf[7] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       epi_l7(acc, D, sm.red, w, lane, mk[7]);
     }
     __syncthreads();
@@ -613,7 +639,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
 #pragma unroll
     for (int l = 7; l >= 1; --l) {
       const int T = D.Kb[l] / 16;
-      gemm_tile<4>(D.Wb[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
+      jac_gemm<JV>(D.Wb[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
       if (l == 4) epi_bwd_l4(acc, sm.H, sm.gin, w, lane, mk[3]);
       else epi_bwd(acc, sm.H, w, lane, mk[l - 1]);

@@ -73,6 +73,64 @@ __device__ __forceinline__ void gemm_tile(const float4* __restrict__ A, int T,
   }
 }
 
+// Same GEMM with the B fragments (LDS) of the next 16-k step loaded before the MFMAs of
+// the current one (+16 VGPRs), so ds_read latency never sits in front of an MFMA.
+template <int NQ, bool PRIO>
+__device__ __forceinline__ void gemm_tile_pf(const float4* __restrict__ A, int T,
+                                             const float* __restrict__ Hs,
+                                             floatx4 (&acc)[NQ][4], int lane) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* Bp = Hs + (lane & 15) * PITCH + 4 * (lane >> 4);
+  float4 a0[NQ], a1[NQ], b0[4], b1[4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) a0[q] = A[(q * T) * 64 + lane];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) b0[cb] = *reinterpret_cast<const float4*>(Bp + cb * 16 * PITCH);
+  for (int t = 0; t < T; t += 2) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) a1[q] = A[(q * T + t + 1) * 64 + lane];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      b1[cb] = *reinterpret_cast<const float4*>(Bp + cb * 16 * PITCH + 16 * (t + 1));
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    mfma_step<NQ>(a0, b0, acc);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    const int tn = (t + 2 < T) ? t + 2 : T - 1;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) a0[q] = A[(q * T + tn) * 64 + lane];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      b0[cb] = *reinterpret_cast<const float4*>(Bp + cb * 16 * PITCH + 16 * tn);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    mfma_step<NQ>(a1, b1, acc);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// Soft barrier among the workgroups that share the label blockIdx % 8 (the dispatcher's
+// XCD round robin, MI355X_MICROARCH.md §Workgroup dispatch): keeps each XCD's workgroups
+// on the same layer so the layer's 1 MB of weights is an L2 hit for all but the first.
+// Purely a speed device: no data is handed over, the spin is bounded, and a wrong
+// placement guess only costs time.
+__device__ __forceinline__ void group_soft_sync(unsigned* ctr, int round) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int g = blockIdx.x & 7;
+    const unsigned gs = (gridDim.x - g + 7) / 8;
+    unsigned* c = ctr + g * 32;
+    const unsigned target = (unsigned)(round + 1) * gs;
+    atomicAdd(c, 1u);
+    for (int spin = 0; spin < (1 << 16); ++spin) {
+      if (atomicAdd(c, 0u) >= target) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  __syncthreads();
+}
+
 // ReLU that keeps torch's NaN propagation (torch.relu(nan) == nan).
 __device__ __forceinline__ float relu_t(float a) { return a > 0.f ? a : (a == a ? 0.f : a); }
 // threshold_backward keeps the gradient where NOT (out <= 0)
