@@ -16,7 +16,7 @@
 #include "dsr_kernels.hpp"
 
 #ifndef DSR_DEFAULT_FWD_VARIANT
-#define DSR_DEFAULT_FWD_VARIANT 6   // B prefetch + s_setprio (A/B: tools/fwd_variants.py)
+#define DSR_DEFAULT_FWD_VARIANT 12  // split-fp16 (3xFP16) + s_setprio (A/B: tools/fwd_variants.py)
 #endif
 
 using namespace dsr;
@@ -33,12 +33,14 @@ struct dsr_ctx {
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                            const float*, float*, unsigned*);
 static FwdKernel fwd_kernel(int v) {
-  switch (v & 7) {
+  switch (v & 15) {
     case 1: return k_mlp_fwd<1>;
     case 2: return k_mlp_fwd<2>;
     case 3: return k_mlp_fwd<3>;
     case 6: return k_mlp_fwd<6>;
     case 7: return k_mlp_fwd<7>;
+    case 8: return k_mlp_fwd16<false>;
+    case 12: return k_mlp_fwd16<true>;
     default: return k_mlp_fwd<0>;
   }
 }
@@ -167,6 +169,31 @@ static void pack_frag(std::vector<float>& out, int rows_pad, int cols_pad,
               src(16 * rb + (lane & 15), 16 * t + 4 * (lane >> 4) + j);
 }
 
+// Split-fp16 A fragments for v_mfma_f32_16x16x32_f16 (dsr_mlp16.hpp):
+// out[(((rb*T + t)*2 + piece)*64 + lane)*8 + j] = piece of src(16 rb + (lane&15), 32 t + 8 (lane>>4) + j) * 2^sw
+static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
+                       const std::function<float(int, int)>& src) {
+  float mx = 0.f;
+  for (int r = 0; r < rows_pad; ++r)
+    for (int c = 0; c < cols_pad; ++c) mx = std::max(mx, std::fabs(src(r, c)));
+  int e = 0;
+  if (mx > 0.f) (void)std::frexp(mx, &e);
+  const int sw = 14 - e;                            // max |W| * 2^sw < 2^14
+  const int RB = rows_pad / 16, T = cols_pad / 32;
+  out.assign((size_t)RB * T * 2 * 64 * 8, (_Float16)0.f);
+  for (int rb = 0; rb < RB; ++rb)
+    for (int t = 0; t < T; ++t)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const float x = std::ldexp(src(16 * rb + (lane & 15), 32 * t + 8 * (lane >> 4) + j), sw);
+          const _Float16 h = (_Float16)x;
+          const _Float16 l = (_Float16)(x - (float)h);
+          out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = h;
+          out[((((size_t)rb * T + t) * 2 + 1) * 64 + lane) * 8 + j] = l;
+        }
+  return sw;
+}
+
 int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, size_t n_floats,
                      dsr_decoder** out) {
   if (!ctx || !d || !w || !out) return fail(ctx, "null argument");
@@ -205,6 +232,23 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   };
   int hf[8] = {-1}, hb[8] = {-1}, hbias[8] = {-1};
   int Kf[8] = {0}, Kb[8] = {0};
+  // split-fp16 forward fragments (stored as raw float storage in the same blob)
+  int hf16[8] = {-1}, sw16[8] = {0};
+  for (int l = 1; l <= 7; ++l) {
+    std::vector<_Float16> v16;
+    if (l == 3) {
+      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return r < L3_OUT ? Wat(3, r, c) : 0.f; });
+    } else if (l == 4) {
+      sw16[l] = pack_frag16(v16, 512, 448, [&](int r, int c) {
+        return c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
+      });
+    } else {
+      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); });
+    }
+    std::vector<float> as_f((v16.size() + 1) / 2);
+    std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
+    hf16[l] = add(std::move(as_f));
+  }
   for (int l = 1; l <= 7; ++l) {
     std::vector<float> v;
     if (l == 3) {
@@ -284,6 +328,10 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   D.W4z = P(h4z);
   D.W8 = P(h8);
   D.b8 = B[8][0];
+  for (int l = 0; l < 8; ++l) {
+    D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
+    D.sw[l] = sw16[l];
+  }
   *out = dec;
   return 0;
 }
@@ -628,7 +676,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
                        (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr);
   } else {
-    hipLaunchKernelGGL(k_mlp_fwd<0>, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+    hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
                        (unsigned*)nullptr);
   }

@@ -45,6 +45,10 @@ struct DevDecoder {
   const float* W4z;      // [512][64] lin4 code columns (folded into a per-object bias)
   const float* W8;       // [512]     lin8 row
   float b8;
+  // split-fp16 copies of the forward A-fragments (dsr_mlp16.hpp):
+  // [32 rb][K/32][2 pieces (hi, lo)][64 lanes] x 8 halfs, scaled by 2^sw[l]
+  const _Float16* Wh_raw[8];
+  int sw[8];
 };
 
 struct ObjDesc {

@@ -19,6 +19,7 @@
 #pragma once
 #include "dsr_dev.hpp"
 #include "dsr_mlp.hpp"
+#include "dsr_mlp16.hpp"
 #include "../../include/dsr.h"
 
 namespace dsr {

@@ -1,0 +1,274 @@
+// dsr_mlp16.hpp — the decoder forward on split-fp16 MFMA ("3xFP16"), fp32-class accuracy.
+//
+// Every fp32 GEMM operand x is carried as two IEEE fp16 pieces, x*2^s = hi + lo with
+// hi = fp16(x*2^s), lo = fp16(x*2^s - hi) (power-of-two scale s, exact), and
+//     A.B = 2^-(sa+sb) (A_hi.B_hi + A_hi.B_lo + A_lo.B_hi)
+// on v_mfma_f32_16x16x32_f16 with fp32 accumulation.  Each piece holds 11 significant
+// bits, so the pair carries 22; products of fp16 are exact in fp32, the dropped
+// A_lo.B_lo term is ~2^-22 relative — the same construction as 3xTF32 (TF32 also has
+// an 11-bit significand), i.e. fp32-class results at 3 MFMAs of 16 cycles per
+// 16x16x32 block versus 8 f32 MFMAs of 32 cycles: 5.3x the fp32 MFMA rate.
+// Scales: weights per layer at load time (max |W| * 2^sw < 2^15), activations per tile
+// and layer from the tile's own max (computed in the epilogue, one LDS max-reduction
+// that rides on the barrier the epilogue already has) — so no input can overflow fp16
+// and small values keep their relative precision.
+//
+// Layout: LDS holds two images Hh/Hl [64 points][528 halfs] (pitch 528: conflict-free
+// ds_read_b128 B-fragment reads).  A fragments are pre-packed per (row block, 32-k step,
+// piece): one 1 KiB coalesced wave-load each.  Wave w owns rows 64w..64w+63 as 4x4
+// 16x16 accumulators, exactly like the fp32 kernel (dsr_mlp.hpp), so the epilogues and
+// the lin8 fusion are shared in structure.
+#pragma once
+#include "dsr_dev.hpp"
+#include "dsr_mlp.hpp"
+
+namespace dsr {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+
+constexpr int PH = 528;                      // LDS pitch of the fp16 images (halfs)
+
+struct Fwd16Shared {
+  _Float16 Hh[TILE * PH];
+  _Float16 Hl[TILE * PH];
+  float xyz[TILE * 4];
+  float red[NWAVE * TILE];
+  float wmax[NWAVE];
+};
+
+// one 32-k step of the 3-product MFMA block for a 64x64 wave tile
+template <bool PRIO>
+__device__ __forceinline__ void mfma3_step(const half8 (&ah)[4], const half8 (&al)[4], const half8 (&bh)[4],
+                                           const half8 (&bl)[4], floatx4 (&acc)[4][4]) {
+  if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q], bh[cb], acc[q][cb], 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bl[cb], acc[q][cb], 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bh[cb], acc[q][cb], 0, 0, 0);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+// acc = A(64 rows of this wave) . H (64 points), K = 32*T.  A: packed [(q*T + t)*2 + piece][lane].
+template <bool PRIO>
+__device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
+                                            const _Float16* Hl, floatx4 (&acc)[4][4], int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const _Float16* Bh = Hh + boff;
+  const _Float16* Bl = Hl + boff;
+  half8 ah0[4], al0[4], ah1[4], al1[4], bh0[4], bl0[4], bh1[4], bl1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ah0[q] = A[((q * T) * 2 + 0) * 64 + lane];
+    al0[q] = A[((q * T) * 2 + 1) * 64 + lane];
+  }
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH);
+    bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH);
+  }
+  for (int t = 0; t < T; t += 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ah1[q] = A[((q * T + t + 1) * 2 + 0) * 64 + lane];
+      al1[q] = A[((q * T + t + 1) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      bh1[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 1));
+      bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
+    }
+    mfma3_step<PRIO>(ah0, al0, bh0, bl0, acc);
+    const int tn = (t + 2 < T) ? t + 2 : T - 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ah0[q] = A[((q * T + tn) * 2 + 0) * 64 + lane];
+      al0[q] = A[((q * T + tn) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * tn);
+      bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * tn);
+    }
+    mfma3_step<PRIO>(ah1, al1, bh1, bl1, acc);
+  }
+}
+
+// power-of-two scale exponent s such that m * 2^s < 2^14 (m >= 0); 0 for m == 0 / non-finite
+__device__ __forceinline__ int act_scale_exp(float m) {
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+  int e;
+  (void)frexpf(m, &e);               // m = f 2^e, f in [0.5, 1)
+  return 14 - e;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Write the wave's 64x64 block of fp32 activations (acc layout, v[q][cb][r]) as hi/lo
+// fp16 pieces scaled by 2^s.
+__device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _Float16* Hh, _Float16* Hl,
+                                            int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 64 * w + 16 * q + 4 * g;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int p = 16 * cb + c;
+      half4 hh, hl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = ldexpf(v[q][cb][r], s);
+        const _Float16 h = (_Float16)x;
+        hh[r] = h;
+        hl[r] = (_Float16)(x - (float)h);
+      }
+      *reinterpret_cast<half4*>(Hh + p * PH + n0) = hh;
+      *reinterpret_cast<half4*>(Hl + p * PH + n0) = hl;
+    }
+  }
+}
+
+// Shared epilogue: v = relu(acc * 2^-unscale + bias) (+ xyz rows for lin3), block max,
+// one barrier, scale, split-write.  Returns the new activation scale exponent.
+__device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
+                                     Fwd16Shared& sm, int w, int lane, bool is_l3) {
+  const int g = lane >> 4, c = lane & 15;
+  float v[4][4][4];
+  float m = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 64 * w + 16 * q + 4 * g;
+    const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int p = 16 * cb + c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = relu_t(ldexpf(accr(acc[q][cb], r), -unscale) + fetch4(bb, r));
+        if (is_l3 && n0 == 444 && r > 0) x = sm.xyz[p * 4 + (r - 1)];
+        v[q][cb][r] = x;
+        m = fmaxf(m, fabsf(x));
+      }
+    }
+  }
+  m = wave_max(m);
+  if (lane == 0) sm.wmax[w] = m;
+  __syncthreads();                       // all waves done reading H; maxima published
+  float mm = sm.wmax[0];
+#pragma unroll
+  for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
+  const int s = act_scale_exp(mm);
+  write_split(v, s, sm.Hh, sm.Hl, w, lane);
+  return s;
+}
+
+template <bool PRIO>
+__global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __restrict__ tiles,
+                                                   const int* __restrict__ n_tiles,
+                                                   const ObjDesc* __restrict__ desc,
+                                                   const float4* __restrict__ cand,
+                                                   const float* __restrict__ bias0f,
+                                                   const float* __restrict__ bias4f,
+                                                   float* __restrict__ dense, unsigned* __restrict__) {
+  __shared__ Fwd16Shared sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int nt = *n_tiles;
+  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+    const Tile tl = tiles[ti];
+    const ObjDesc d = desc[tl.obj];
+    if (tid < TILE) {
+      const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+      sm.xyz[tid * 4 + 0] = v.x; sm.xyz[tid * 4 + 1] = v.y;
+      sm.xyz[tid * 4 + 2] = v.z; sm.xyz[tid * 4 + 3] = v.w;
+    }
+    __syncthreads();
+    // ---- lin0 on VALU (fp32), then split
+    int sa;
+    {
+      const float* bias0 = bias0f + tl.obj * HID;
+      float v[4][4][4];
+      float m = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
+        float wx[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
+          const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+            v[q][cb][r] = relu_t(a);
+            m = fmaxf(m, fabsf(v[q][cb][r]));
+          }
+        }
+      }
+      m = wave_max(m);
+      if (lane == 0) sm.wmax[w] = m;
+      __syncthreads();
+      float mm = sm.wmax[0];
+#pragma unroll
+      for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
+      sa = act_scale_exp(mm);
+      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+    }
+    __syncthreads();
+    floatx4 acc[4][4];
+    for (int l = 1; l <= 6; ++l) {
+      const int T = D.Kf[l] / 32;
+      gemm16_tile<PRIO>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
+      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
+      __syncthreads();
+    }
+    {
+      const int T = D.Kf[7] / 32;
+      gemm16_tile<PRIO>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
+      const int un = D.sw[7] + sa;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
+      uint64_t mask;
+      epi_l7(acc, D, sm.red, w, lane, mask);
+    }
+    __syncthreads();
+    if (tid < tl.count) {
+      float s = sm.red[tid];
+      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+      const float y = tanhf(s + D.b8);
+      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
+      dense[d.cand_off + idx] = y;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace dsr
