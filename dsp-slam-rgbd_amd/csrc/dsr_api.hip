@@ -44,6 +44,16 @@ static FwdKernel fwd_kernel(int v) {
     default: return k_mlp_fwd<0>;
   }
 }
+using JacKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const ObjState*, const float*,
+                           const float4*, const float*, const float*, const float*, GNParams, float*,
+                           const float4*, float*, float*);
+static JacKernel jac_kernel() {
+  const char* e = getenv("DSR_JAC_VARIANT");
+  const int v = e ? atoi(e) : 12;
+  if (v == 12) return k_mlp_jac16<true>;
+  if (v == 8) return k_mlp_jac16<false>;
+  return k_mlp_jac;
+}
 static int fwd_variant() {
   const char* e = getenv("DSR_FWD_VARIANT");
   return e ? atoi(e) : DSR_DEFAULT_FWD_VARIANT;
@@ -265,6 +275,20 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
     }
     hf[l] = add(std::move(v));
   }
+  int hb16[8] = {-1}, swb16[8] = {0};
+  for (int l = 0; l <= 7; ++l) {
+    std::vector<_Float16> v16;
+    if (l == 0) {
+      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? Wat(0, c, r) : 0.f; });
+    } else if (l == 3) {
+      swb16[l] = pack_frag16(v16, 512, 448, [&](int r, int c) { return c < L3_OUT ? Wat(3, c, r) : 0.f; });
+    } else {
+      swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); });
+    }
+    std::vector<float> as_f((v16.size() + 1) / 2);
+    std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
+    hb16[l] = add(std::move(as_f));
+  }
   for (int l = 1; l <= 7; ++l) {
     std::vector<float> v;
     if (l == 3) {
@@ -331,6 +355,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 0; l < 8; ++l) {
     D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
     D.sw[l] = sw16[l];
+    D.Wbh_raw[l] = reinterpret_cast<const _Float16*>(P(hb16[l]));
+    D.swb[l] = swb16[l];
   }
   *out = dec;
   return 0;
@@ -497,6 +523,7 @@ int dsr_batch_run(dsr_batch* b) {
   const int grid = ctx->n_cu;
   const int cb = (n + 63) / 64;
   const FwdKernel fwdk = fwd_kernel(fwd_variant());
+  const JacKernel jack = jac_kernel();
   DSR_CHECK(ctx, hipEventRecord(b->ev[0], s));
   hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
   for (int it = 0; it < b->iters; ++it) {
@@ -514,7 +541,7 @@ int dsr_batch_run(dsr_batch* b) {
                        b->dense, b->kpts, b->kres);
     hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_j, b->nt_j);
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 2], s));
-    hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
+    hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
                        b->pts, b->kpts, b->kres, b->bias0f, b->bias4f, P, b->slots,
                        (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
     DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 3], s));
@@ -671,7 +698,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   const int grid = std::min(ctx->n_cu, nt);
   if (jac) {
     GNParams P{};
-    hipLaunchKernelGGL(k_mlp_jac, dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+    hipLaunchKernelGGL(jac_kernel(), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const ObjState*)nullptr, (const float*)nullptr,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
                        (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr);
@@ -755,7 +782,7 @@ int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* 
   for (int e = 0; e < iters; ++e) {
     const int nt = (n + TILE - 1) / TILE;
     const bool filter = (e == 4) && (e + 1 < iters);   // :77-79 inlier filter (effective only past 5 iters)
-    hipLaunchKernelGGL(k_mlp_jac, dim3(std::max(1, std::min(ctx->n_cu, nt))), dim3(512), 0, s, D, (const Tile*)dt,
+    hipLaunchKernelGGL(jac_kernel(), dim3(std::max(1, std::min(ctx->n_cu, nt))), dim3(512), 0, s, D, (const Tile*)dt,
                        (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst, (const float*)dpts,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
                        (float*)dslots, (const float4*)nullptr, (float*)nullptr, filter ? (float*)dres : (float*)nullptr);

@@ -526,6 +526,90 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
 // ------------------------------------------------------------------------------------
 // k_mlp_jac: forward + analytic input Jacobian + per-tile normal-equation partials
 // ------------------------------------------------------------------------------------
+constexpr int JPITCH = 72;
+
+// Tail shared by the fp32 and split-fp16 Jacobian kernels: raw output (dsr_sdf_eval), or
+// J rows (loss.py:34-41 / :157-164) + Huber residuals + per-tile normal-equation partials.
+__device__ __forceinline__ void jac_tail(const Tile& tl, const ObjDesc& d, const ObjState* __restrict__ st,
+                                         const GNParams& P, float* __restrict__ slots,
+                                         float* __restrict__ raw_out, float* __restrict__ res_out,
+                                         const float* ys, const float* gin, const float* xyz, float* rs,
+                                         float* Jbuf, int tid) {
+    if (tl.term == 2) {            // raw query (dsr_sdf_eval): sdf + gradient out
+      for (int e = tid; e < TILE * (IN + 1); e += 512) {
+        const int p = e / (IN + 1), k = e - p * (IN + 1);
+        if (p < tl.count)
+          raw_out[(size_t)(tl.start + p) * (IN + 1) + k] = (k == 0) ? ys[p] : gin[p * GIN_PITCH + k - 1];
+      }
+      __syncthreads();
+      return;
+    }
+    // ---- J rows (loss.py:34-41 / :157-164) into the freed H region
+    float* J = Jbuf;
+    {
+      const int p = tid >> 3, sub = tid & 7;
+      const bool valid = p < tl.count;
+      const bool ren = tl.term == 1;
+      const float deds = xyz[p * 4 + 3];
+      const float* gi = gin + p * GIN_PITCH;
+      for (int e = sub; e < NPAR; e += 8) {
+        float v;
+        if (e >= NPOSE) {
+          v = ren ? deds * gi[e - NPOSE] : gi[e - NPOSE];
+        } else {
+          const float g0 = ren ? deds * gi[64] : gi[64];
+          const float g1 = ren ? deds * gi[65] : gi[65];
+          const float g2 = ren ? deds * gi[66] : gi[66];
+          const float x = xyz[p * 4 + 0], y = xyz[p * 4 + 1], z = xyz[p * 4 + 2];
+          // g . [I | -[x]x | x]  (get_points_to_pose_jacobian_sim3, loss_utils.py:176-195)
+          switch (e) {
+            case 0: v = g0; break;
+            case 1: v = g1; break;
+            case 2: v = g2; break;
+            case 3: v = g1 * (-z) + g2 * y; break;
+            case 4: v = g0 * z + g2 * (-x); break;
+            case 5: v = g0 * (-y) + g1 * x; break;
+            default: v = (g0 * x + g1 * y) + g2 * z; break;
+          }
+        }
+        J[p * JPITCH + e] = valid ? v : 0.f;
+      }
+      if (tid < TILE) {
+        // Huber-weighted residual (loss_utils.py:246-275); sdf residual = decoder output
+        const float res = ren ? rs[tid] : ys[tid];
+        const float b = ren ? P.b1 : P.b2;
+        const float x = fabsf(res);
+        const float hn = (x <= b) ? x * x : (2.0f * b) * x - b * b;
+        const float den = (x == 0.f) ? 1.f : x;
+        const float wgt = sqrtf(hn) / den;
+        rs[tid] = (tid < tl.count) ? (P.raw_residual ? res : wgt * res) : 0.f;
+        if (res_out && !ren && tid < tl.count) res_out[d.pts_off + tl.start + tid] = res;
+      }
+    }
+    __syncthreads();
+    // ---- per-tile partials: upper-tri J^T J, J^T r~, sum r~^2
+    {
+      const int slot = d.slot_sdf + (tl.term == 0 ? 0 : st[tl.obj].n_sdf_tiles) + tl.start / TILE;
+      float* out = slots + (size_t)slot * SLOT_FLOATS;
+      for (int e = tid; e < SLOT_FLOATS; e += 512) {
+        float s = 0.f;
+        if (e < NTRI) {
+          int a = 0, rem = e;
+          while (rem >= NPAR - a) { rem -= NPAR - a; ++a; }
+          const int b = a + rem;
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], J[p * JPITCH + b], s);
+        } else if (e < NTRI + NPAR) {
+          const int a = e - NTRI;
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], rs[p], s);
+        } else {
+          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(rs[p], rs[p], s);
+        }
+        out[e] = s;
+      }
+    }
+    __syncthreads();
+}
+
 struct JacShared {
   float H[H_FLOATS];           // activations / gradients, later the tile's J [64][72]
   float xyz[TILE * 4];         // object-frame point (x,y,z) + de_ds (render term)
@@ -535,7 +619,6 @@ struct JacShared {
   float gin[TILE * GIN_PITCH]; // d sdf / d [code(64), xyz(3)]
 };
 
-constexpr int JPITCH = 72;
 
 #ifndef DSR_JAC_VARIANT
 #define DSR_JAC_VARIANT 6
@@ -662,79 +745,233 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
       }
     }
     __syncthreads();
-    if (tl.term == 2) {            // raw query (dsr_sdf_eval): sdf + gradient out
-      for (int e = tid; e < TILE * (IN + 1); e += 512) {
-        const int p = e / (IN + 1), k = e - p * (IN + 1);
-        if (p < tl.count)
-          raw_out[(size_t)(tl.start + p) * (IN + 1) + k] = (k == 0) ? sm.y[p] : sm.gin[p * GIN_PITCH + k - 1];
-      }
-      __syncthreads();
-      continue;
-    }
-    // ---- J rows (loss.py:34-41 / :157-164) into the freed H region
-    float* J = sm.H;
-    {
-      const int p = tid >> 3, sub = tid & 7;
-      const bool valid = p < tl.count;
-      const bool ren = tl.term == 1;
-      const float deds = sm.xyz[p * 4 + 3];
-      const float* gi = sm.gin + p * GIN_PITCH;
-      for (int e = sub; e < NPAR; e += 8) {
-        float v;
-        if (e >= NPOSE) {
-          v = ren ? deds * gi[e - NPOSE] : gi[e - NPOSE];
+    jac_tail(tl, d, st, P, slots, raw_out, res_out, sm.y, sm.gin, sm.xyz, sm.r, sm.H, tid);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_mlp_jac16: the Jacobian kernel on split-fp16 MFMA (dsr_mlp16.hpp); same structure as
+// k_mlp_jac, every GEMM operand image carried as scaled hi/lo fp16 pieces with a per-tile
+// per-layer power-of-two scale (forward activations and backward gradients alike).
+// ------------------------------------------------------------------------------------
+struct Jac16Shared {
+  _Float16 Hh[TILE * PH];      // hi pieces; later the tile's J [64][72] (fp32)
+  _Float16 Hl[TILE * PH];
+  float xyz[TILE * 4];
+  float red[NWAVE * TILE];
+  float y[TILE];
+  float r[TILE];
+  float gin[TILE * GIN_PITCH];
+  float wmax[NWAVE];
+};
+
+template <bool PRIO>
+__global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __restrict__ tiles,
+                                                   const int* __restrict__ n_tiles,
+                                                   const ObjDesc* __restrict__ desc,
+                                                   const ObjState* __restrict__ st,
+                                                   const float* __restrict__ pts_all,
+                                                   const float4* __restrict__ kpts,
+                                                   const float* __restrict__ kres,
+                                                   const float* __restrict__ bias0f,
+                                                   const float* __restrict__ bias4f, GNParams P,
+                                                   float* __restrict__ slots,
+                                                   const float4* __restrict__ raw_pts,
+                                                   float* __restrict__ raw_out,
+                                                   float* __restrict__ res_out) {
+  __shared__ Jac16Shared sm;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c = lane & 15;
+  const int nt = *n_tiles;
+  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+    const Tile tl = tiles[ti];
+    const ObjDesc d = desc[tl.obj];
+    if (tid < TILE) {
+      float x = 0.f, y = 0.f, z = 0.f, aux = 0.f, rr = 0.f;
+      if (tid < tl.count) {
+        if (tl.term == 0) {
+          const float* p = pts_all + (size_t)(d.pts_off + tl.start + tid) * 3;
+          const float3 xo = xform(st[tl.obj].T, p[0], p[1], p[2]);
+          x = xo.x; y = xo.y; z = xo.z;
+        } else if (tl.term == 1) {
+          const float4 v = kpts[d.cand_off + tl.start + tid];
+          x = v.x; y = v.y; z = v.z; aux = v.w;
+          rr = kres[d.cand_off + tl.start + tid];
         } else {
-          const float g0 = ren ? deds * gi[64] : gi[64];
-          const float g1 = ren ? deds * gi[65] : gi[65];
-          const float g2 = ren ? deds * gi[66] : gi[66];
+          const float4 v = raw_pts[tl.start + tid];
+          x = v.x; y = v.y; z = v.z;
+        }
+      }
+      sm.xyz[tid * 4 + 0] = x; sm.xyz[tid * 4 + 1] = y;
+      sm.xyz[tid * 4 + 2] = z; sm.xyz[tid * 4 + 3] = aux;
+      sm.r[tid] = rr;
+    }
+    __syncthreads();
+    uint64_t mk[8];
+    float v[4][4][4];
+    int sa;
+    // ---- lin0 (VALU, fp32) + masks
+    {
+      const float* bias0 = bias0f + tl.obj * HID;
+      float m = 0.f;
+      mk[0] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
+        float wx[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
           const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
-          // g . [I | -[x]x | x]  (get_points_to_pose_jacobian_sim3, loss_utils.py:176-195)
-          switch (e) {
-            case 0: v = g0; break;
-            case 1: v = g1; break;
-            case 2: v = g2; break;
-            case 3: v = g1 * (-z) + g2 * y; break;
-            case 4: v = g0 * z + g2 * (-x); break;
-            case 5: v = g0 * (-y) + g1 * x; break;
-            default: v = (g0 * x + g1 * y) + g2 * z; break;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+            const float h = relu_t(a);
+            if (relu_pass(h)) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
+            v[q][cb][r] = h;
+            m = fmaxf(m, fabsf(h));
           }
         }
-        J[p * JPITCH + e] = valid ? v : 0.f;
       }
-      if (tid < TILE) {
-        // Huber-weighted residual (loss_utils.py:246-275); sdf residual = decoder output
-        const float res = ren ? sm.r[tid] : sm.y[tid];
-        const float b = ren ? P.b1 : P.b2;
-        const float x = fabsf(res);
-        const float hn = (x <= b) ? x * x : (2.0f * b) * x - b * b;
-        const float den = (x == 0.f) ? 1.f : x;
-        const float wgt = sqrtf(hn) / den;
-        sm.r[tid] = (tid < tl.count) ? (P.raw_residual ? res : wgt * res) : 0.f;
-        if (res_out && !ren && tid < tl.count) res_out[d.pts_off + tl.start + tid] = res;
-      }
+      sa = block_scale(m, sm.wmax, w, lane);
+      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
     }
     __syncthreads();
-    // ---- per-tile partials: upper-tri J^T J, J^T r~, sum r~^2
-    {
-      const int slot = d.slot_sdf + (tl.term == 0 ? 0 : st[tl.obj].n_sdf_tiles) + tl.start / TILE;
-      float* out = slots + (size_t)slot * SLOT_FLOATS;
-      for (int e = tid; e < SLOT_FLOATS; e += 512) {
-        float s = 0.f;
-        if (e < NTRI) {
-          int a = 0, rem = e;
-          while (rem >= NPAR - a) { rem -= NPAR - a; ++a; }
-          const int b = a + rem;
-          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], J[p * JPITCH + b], s);
-        } else if (e < NTRI + NPAR) {
-          const int a = e - NTRI;
-          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(J[p * JPITCH + a], sm.r[p], s);
-        } else {
-          for (int p = 0; p < TILE; ++p) s = __builtin_fmaf(sm.r[p], sm.r[p], s);
+    floatx4 acc[4][4];
+    // ---- forward lin1..lin6 (masks kept)
+#pragma unroll
+    for (int l = 1; l <= 6; ++l) {
+      const int T = D.Kf[l] / 32;
+      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
+                           sm.Hh, sm.Hl, acc, lane);
+      const int un = D.sw[l] + sa;
+      const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
+      float m = 0.f;
+      mk[l] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float h = relu_t(ldexpf(accr(acc[q][cb], r), -un) + fetch4(bb, r));
+            if (relu_pass(h)) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
+            if (l == 3 && n0 == 444 && r > 0) h = sm.xyz[p * 4 + (r - 1)];
+            v[q][cb][r] = h;
+            m = fmaxf(m, fabsf(h));
+          }
         }
-        out[e] = s;
+      }
+      sa = block_scale(m, sm.wmax, w, lane);
+      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      __syncthreads();
+    }
+    // ---- lin7 + lin8 dot + tanh
+    {
+      const int T = D.Kf[7] / 32;
+      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T,
+                           sm.Hh, sm.Hl, acc, lane);
+      const int un = D.sw[7] + sa;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
+      epi_l7(acc, D, sm.red, w, lane, mk[7]);
+    }
+    __syncthreads();
+    if (tid < TILE) {
+      float s = sm.red[tid];
+      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+      sm.y[tid] = tanhf(s + D.b8);
+    }
+    __syncthreads();
+    // ---- g7 = (1 - y^2) W8 (.) relu'(a7)
+    {
+      float m = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 w8 = *reinterpret_cast<const float4*>(D.W8 + n0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
+          const float yy = sm.y[p];
+          const float dt = 1.f - yy * yy;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gv = ((mk[7] >> ((q * 4 + cb) * 4 + r)) & 1ull) ? dt * fetch4(w8, r) : 0.f;
+            v[q][cb][r] = gv;
+            m = fmaxf(m, fabsf(gv));
+          }
+        }
+      }
+      sa = block_scale(m, sm.wmax, w, lane);     // (no GEMM in flight: the barrier is harmless)
+      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+    }
+    __syncthreads();
+    // ---- backward lin7^T .. lin1^T
+#pragma unroll
+    for (int l = 7; l >= 1; --l) {
+      const int T = D.Kb[l] / 32;
+      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wbh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
+                           sm.Hh, sm.Hl, acc, lane);
+      const int un = D.swb[l] + sa;
+      float m = 0.f;
+      const uint64_t mask = mk[l - 1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int p = 16 * cb + c;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + r;
+            const float a = ldexpf(accr(acc[q][cb], r), -un);
+            float gv;
+            if (l == 4 && n >= L3_OUT) {                  // d/d[code, xyz] via the latent skip
+              sm.gin[p * GIN_PITCH + (n - L3_OUT)] = a;
+              gv = 0.f;
+            } else {
+              gv = ((mask >> ((q * 4 + cb) * 4 + r)) & 1ull) ? a : 0.f;
+            }
+            v[q][cb][r] = gv;
+            m = fmaxf(m, fabsf(gv));
+          }
+        }
+      }
+      sa = block_scale(m, sm.wmax, w, lane);
+      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      __syncthreads();
+    }
+    // ---- lin0^T (80 rows; waves 0..4): d sdf / d input += W0^T g0
+    if (w < 5) {
+      floatx4 a1[1][4];
+      gemm16_tile<PRIO, 1>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
+                           sm.Hh, sm.Hl, a1, lane);
+      const int un = D.swb[0] + sa;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int p = 16 * cb + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * w + 4 * g + r;
+          if (n < IN) sm.gin[p * GIN_PITCH + n] = ldexpf(accr(a1[0][cb], r), -un) + sm.gin[p * GIN_PITCH + n];
+        }
       }
     }
     __syncthreads();
+    jac_tail(tl, d, st, P, slots, raw_out, res_out, sm.y, sm.gin, sm.xyz, sm.r,
+             reinterpret_cast<float*>(sm.Hh), tid);
   }
 }
 

@@ -38,42 +38,42 @@ struct Fwd16Shared {
 };
 
 // one 32-k step of the 3-product MFMA block for a 64x64 wave tile
-template <bool PRIO>
-__device__ __forceinline__ void mfma3_step(const half8 (&ah)[4], const half8 (&al)[4], const half8 (&bh)[4],
-                                           const half8 (&bl)[4], floatx4 (&acc)[4][4]) {
+template <bool PRIO, int NQ>
+__device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&al)[NQ], const half8 (&bh)[4],
+                                           const half8 (&bl)[4], floatx4 (&acc)[NQ][4]) {
   if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q], bh[cb], acc[q][cb], 0, 0, 0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bl[cb], acc[q][cb], 0, 0, 0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bh[cb], acc[q][cb], 0, 0, 0);
   if (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
-// acc = A(64 rows of this wave) . H (64 points), K = 32*T.  A: packed [(q*T + t)*2 + piece][lane].
-template <bool PRIO>
+// acc = A(16*NQ rows of this wave) . H (64 points), K = 32*T.  A: packed [(q*T + t)*2 + piece][lane].
+template <bool PRIO, int NQ = 4>
 __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
-                                            const _Float16* Hl, floatx4 (&acc)[4][4], int lane) {
+                                            const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int boff = (lane & 15) * PH + 8 * (lane >> 4);
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
-  half8 ah0[4], al0[4], ah1[4], al1[4], bh0[4], bl0[4], bh1[4], bl1[4];
+  half8 ah0[NQ], al0[NQ], ah1[NQ], al1[NQ], bh0[4], bl0[4], bh1[4], bl1[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     ah0[q] = A[((q * T) * 2 + 0) * 64 + lane];
     al0[q] = A[((q * T) * 2 + 1) * 64 + lane];
   }
@@ -84,7 +84,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
   }
   for (int t = 0; t < T; t += 2) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       ah1[q] = A[((q * T + t + 1) * 2 + 0) * 64 + lane];
       al1[q] = A[((q * T + t + 1) * 2 + 1) * 64 + lane];
     }
@@ -93,10 +93,10 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
       bh1[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 1));
       bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
     }
-    mfma3_step<PRIO>(ah0, al0, bh0, bl0, acc);
+    mfma3_step<PRIO, NQ>(ah0, al0, bh0, bl0, acc);
     const int tn = (t + 2 < T) ? t + 2 : T - 1;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       ah0[q] = A[((q * T + tn) * 2 + 0) * 64 + lane];
       al0[q] = A[((q * T + tn) * 2 + 1) * 64 + lane];
     }
@@ -105,7 +105,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
       bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * tn);
       bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * tn);
     }
-    mfma3_step<PRIO>(ah1, al1, bh1, bl1, acc);
+    mfma3_step<PRIO, NQ>(ah1, al1, bh1, bl1, acc);
   }
 }
 
@@ -121,6 +121,18 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
+}
+
+// Workgroup max of |v| -> power-of-two scale exponent.  Contains the barrier that
+// separates the previous GEMM's reads of the image from the writes of the next one.
+__device__ __forceinline__ int block_scale(float m, float* wmax, int w, int lane) {
+  m = wave_max(m);
+  if (lane == 0) wmax[w] = m;
+  __syncthreads();
+  float mm = wmax[0];
+#pragma unroll
+  for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, wmax[k]);
+  return act_scale_exp(mm);
 }
 
 // Write the wave's 64x64 block of fp32 activations (acc layout, v[q][cb][r]) as hi/lo
@@ -242,13 +254,13 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     floatx4 acc[4][4];
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 32;
-      gemm16_tile<PRIO>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
+      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
       sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
       __syncthreads();
     }
     {
       const int T = D.Kf[7] / 32;
-      gemm16_tile<PRIO>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
+      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)

@@ -109,7 +109,10 @@ def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
         assert abs(t["loss"][0] - loss_ref) <= tol, (e, dk)
         if dk == 0:
             assert abs(t["render_loss"][0] - f["it_render_loss"][e]) <= 1e-5 * f["it_render_loss"][e]
-            assert abs(t["sdf_loss"][0] - f["it_sdf_loss"][e]) <= 1e-5 * f["it_sdf_loss"][e]
+            # the sdf residuals are surface-point SDFs ~1e-2 while any fp32 decoder is off
+            # by ~1e-7 absolute (numpy fp32 vs fp64: rms 7.6e-8, tools/diag_precision.py),
+            # so mean(r^2) carries ~2e-5 relative noise in every fp32 implementation
+            assert abs(t["sdf_loss"][0] - f["it_sdf_loss"][e]) <= 5e-5 * f["it_sdf_loss"][e]
         assert rel(t["H"][0], f["it_H"][e]) <= 2e-3, e
         # b[3:6] carries k4 * J_rot * r_rot with k4 = 1e7 and r_rot = 1 - cos(tilt), an fp32
         # cancellation in the reference itself: max-norm loose, step in the H-norm tight
@@ -131,13 +134,13 @@ def test_trajectory_shadowing_and_final(gpu_decoder, oracle_dec, name, optim, dt
     (r,), (t,) = opt.reconstruct_objects(
         [(f["obj_t_cam_obj"], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)], trace=True)
     assert r["is_good"]
-    # final loss inside the reference's own ensemble (1/2/4/8 threads, 1-ulp pose
-    # perturbations), widened by the ensemble's width (min 1% of the loss)
+    # final loss vs the reference, judged against the reference's own spread: its
+    # ensemble (1/2/4/8 threads, 1-ulp pose perturbations) moves the final loss by up to
+    # `dev`; a chaotic fp32 trajectory is accepted within 3 dev (min 1% of the loss).
+    # Per-step correctness is proved below by shadowing, not by this bound.
     ref = float(f["loss"])
-    ens = np.concatenate([[ref], f["ens_loss"]])
-    lo, hi = ens.min(), ens.max()
-    pad = max(hi - lo, 0.01 * abs(ref))
-    assert lo - pad <= r["loss"] <= hi + pad, (r["loss"], lo, hi)
+    dev = float(np.abs(f["ens_loss"] - ref).max())
+    assert abs(r["loss"] - ref) <= max(3 * dev, 0.01 * abs(ref)), (r["loss"], ref, dev)
     # shadowing: the GPU's step e, re-taken from the state the GPU itself reached, vs
     # the oracle's step from that same state
     P = O.OptimParams.from_cfg(optim)
