@@ -830,8 +830,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
-            const float h = relu_t(a);
-            if (relu_pass(h)) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
+            const float h = fmaxf(a, 0.f);            // NaN re-imposed after the backward
+            if (h > 0.f) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
             v[q][cb][r] = h;
             m = fmaxf(m, fabsf(h));
           }
@@ -843,12 +843,12 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     __syncthreads();
     floatx4 acc[4][4];
     // ---- forward lin1..lin6 (masks kept)
-#pragma unroll
+#pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 32;
       gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
                            sm.Hh, sm.Hl, acc, lane);
-      const int un = D.sw[l] + sa;
+      const float usc = ldexpf(1.f, -(D.sw[l] + sa));
       const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
       float m = 0.f;
       mk[l] = 0;
@@ -861,8 +861,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           const int p = 16 * cb + c;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float h = relu_t(ldexpf(accr(acc[q][cb], r), -un) + fetch4(bb, r));
-            if (relu_pass(h)) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
+            float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+            if (h > 0.f) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
             if (l == 3 && n0 == 444 && r > 0) h = sm.xyz[p * 4 + (r - 1)];
             v[q][cb][r] = h;
             m = fmaxf(m, fabsf(h));
@@ -919,12 +919,12 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     }
     __syncthreads();
     // ---- backward lin7^T .. lin1^T
-#pragma unroll
+#pragma unroll 1
     for (int l = 7; l >= 1; --l) {
       const int T = D.Kb[l] / 32;
       gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wbh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
                            sm.Hh, sm.Hl, acc, lane);
-      const int un = D.swb[l] + sa;
+      const float usc = ldexpf(1.f, -(D.swb[l] + sa));
       float m = 0.f;
       const uint64_t mask = mk[l - 1];
 #pragma unroll
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int n = n0 + r;
-            const float a = ldexpf(accr(acc[q][cb], r), -un);
+            const float a = accr(acc[q][cb], r) * usc;    // exact (power of two)
             float gv;
             if (l == 4 && n >= L3_OUT) {                  // d/d[code, xyz] via the latent skip
               sm.gin[p * GIN_PITCH + (n - L3_OUT)] = a;
@@ -967,6 +967,16 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           const int n = 16 * w + 4 * g + r;
           if (n < IN) sm.gin[p * GIN_PITCH + n] = ldexpf(accr(a1[0][cb], r), -un) + sm.gin[p * GIN_PITCH + n];
         }
+      }
+    }
+    // torch.relu propagates NaN; the v_max ReLUs above do not, and a NaN can only come in
+    // through the point or the code: re-impose it on the outputs of such points
+    if (tid < TILE) {
+      const float px = sm.xyz[tid * 4 + 0], py = sm.xyz[tid * 4 + 1], pz = sm.xyz[tid * 4 + 2];
+      const float zprobe = bias0f[tl.obj * HID];
+      if (px != px || py != py || pz != pz || zprobe != zprobe) {
+        sm.y[tid] = __builtin_nanf("");
+        for (int e = 0; e < IN; ++e) sm.gin[tid * GIN_PITCH + e] = __builtin_nanf("");
       }
     }
     __syncthreads();

@@ -165,6 +165,7 @@ __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _F
 __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
                                      Fwd16Shared& sm, int w, int lane, bool is_l3) {
   const int g = lane >> 4, c = lane & 15;
+  const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
   float m = 0.f;
 #pragma unroll
@@ -176,10 +177,12 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
       const int p = 16 * cb + c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float x = relu_t(ldexpf(accr(acc[q][cb], r), -unscale) + fetch4(bb, r));
+        // acc*2^-unscale is exact, so the fma rounds exactly like (acc*2^-un) + b; ReLU as
+        // v_max (NaN inputs are re-imposed on the output, see nan_in below)
+        float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
         if (is_l3 && n0 == 444 && r > 0) x = sm.xyz[p * 4 + (r - 1)];
         v[q][cb][r] = x;
-        m = fmaxf(m, fabsf(x));
+        m = fmaxf(m, x);                  // x >= 0
       }
     }
   }
@@ -236,8 +239,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
-            v[q][cb][r] = relu_t(a);
-            m = fmaxf(m, fabsf(v[q][cb][r]));
+            v[q][cb][r] = fmaxf(a, 0.f);
+            m = fmaxf(m, v[q][cb][r]);
           }
         }
       }
@@ -275,7 +278,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     if (tid < tl.count) {
       float s = sm.red[tid];
       for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
-      const float y = tanhf(s + D.b8);
+      float y = tanhf(s + D.b8);
+      // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
+      // enter through the point or the code, so re-impose it here
+      const float px = sm.xyz[tid * 4 + 0], py = sm.xyz[tid * 4 + 1], pz = sm.xyz[tid * 4 + 2];
+      const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
+      if (px != px || py != py || pz != pz || zprobe != zprobe) y = __builtin_nanf("");
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
       dense[d.cand_off + idx] = y;
     }

@@ -323,3 +323,22 @@ def test_sharded_two_ranks_on_device(gpu_decoder):
         assert good and r["is_good"]
         assert np.float32(loss) == np.float32(r["loss"])
         assert np.array_equal(np.asarray(T, np.float32), r["t_cam_obj"])
+
+
+def test_nan_propagation(gpu_decoder):
+    """torch.relu propagates NaN (deep_sdf_decoder.py:103): a NaN point or code gives a NaN
+    SDF, every other point of the same tile stays finite and unchanged."""
+    from reconstruct.optimizer import sdf_eval
+
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-0.8, 0.8, (100, 3)).astype(np.float32)
+    z = (0.05 * rng.standard_normal(64)).astype(np.float32)
+    y0 = sdf_eval(gpu_decoder, z, x)
+    x2 = x.copy()
+    x2[7, 1] = np.nan
+    y1 = sdf_eval(gpu_decoder, z, x2)
+    assert np.isnan(y1[7]) and np.isfinite(np.delete(y1, 7)).all()
+    assert np.abs(np.delete(y1, 7) - np.delete(y0, 7)).max() <= 1e-6
+    z2 = z.copy()
+    z2[3] = np.nan
+    assert np.isnan(sdf_eval(gpu_decoder, z2, x)).all()
