@@ -99,7 +99,7 @@ def cpu_baseline(seconds_budget=30.0):
 
 
 def pmc_traffic():
-    """HBM bytes per k_mlp_fwd launch from the newest committed rocprofv3 PMC summary
+    """HBM bytes per k_mlp_fwd16 launch from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_summary.json, written by tools/prof_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes over this same default workload), or None."""
     import glob
@@ -108,10 +108,11 @@ def pmc_traffic():
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json")), key=os.path.getmtime):
         try:
             d = json.load(open(f))
-            v = d["pmc"]["k_mlp_fwd"]["hbm_bytes_per_launch"]
-            best = (v, os.path.relpath(f, REPO))
         except Exception:
             continue
+        for name, e in d.get("pmc", {}).items():
+            if "k_mlp_fwd16" in name and "hbm_bytes_per_launch" in e:
+                best = (e["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
     return best
 
 
@@ -174,7 +175,7 @@ def main():
     ctx.check(lib.dsr_batch_sync(batch), "sync")
     t0 = time.perf_counter()
     fwd_ms = jac_ms = 0.0
-    fwd_pts = jac_pts = 0
+    fwd_pts = jac_pts = inball_pts = fwd_launches = 0
     n_good = 0
     for _ in range(args.steps):
         step()
@@ -184,6 +185,8 @@ def main():
         jac_ms += st.jac_ms
         fwd_pts += st.fwd_points
         jac_pts += st.jac_points
+        inball_pts += st.inball_points
+        fwd_launches += st.fwd_launches
         n_good += sum(int(outs[i].is_good) for i in range(n_obj))
     ctx.check(lib.dsr_batch_sync(batch), "sync")
     if dist is not None:
@@ -238,8 +241,11 @@ def main():
                          "unit": "TFLOP/s", "frac": round(fwd_tf / peak_tf, 4),
                          "peak_note": peak_note,
                          "traffic": None, "traffic_unit": "bytes/launch (HBM+MALL, PMC)",
-                         "flop_per_launch": fwd_flop / max(1, args.steps * 10),
-                         "avg_launch_ms": fwd_ms / max(1, args.steps * 10)},
+                         "launches": fwd_launches,
+                         "flop_per_launch": fwd_flop / max(1, fwd_launches),
+                         "avg_launch_ms": fwd_ms / max(1, fwd_launches)},
+            "early_ray_termination": {"samples_decoded": fwd_pts, "samples_in_ball": inball_pts,
+                                      "decoded_fraction": round(fwd_pts / max(1, inball_pts), 4)},
             "job_tflops": round(job_tf, 3),
             "jac_kernel_tflops": round(jac_flop / (jac_ms * 1e-3) / 1e12, 3) if jac_ms > 0 else 0.0,
             "good_fraction": n_good / float(n_obj * args.steps),

@@ -29,9 +29,11 @@ struct dsr_ctx {
   std::string err;
 };
 
-// Forward-kernel variant (DSR_FWD_VARIANT, bit0 XCD soft sync, bit1 B prefetch, bit2 setprio)
+// Forward-kernel variant (DSR_FWD_VARIANT, bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
+// bit3 split-fp16, bit4 cross-layer A prefetch (split-fp16 only); 12+32 / 12+64 are timing
+// experiments with a reduced / no epilogue (invalid results))
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
-                           const float*, float*, unsigned*);
+                           const float*, float*, unsigned*, ErtArgs);
 static FwdKernel fwd_kernel(int v) {
   switch (v & 15) {
     case 1: return k_mlp_fwd<1>;
@@ -39,8 +41,14 @@ static FwdKernel fwd_kernel(int v) {
     case 3: return k_mlp_fwd<3>;
     case 6: return k_mlp_fwd<6>;
     case 7: return k_mlp_fwd<7>;
-    case 8: return k_mlp_fwd16<false>;
-    case 12: return k_mlp_fwd16<true>;
+    case 8: return (v & 16) ? k_mlp_fwd16<false, 1> : k_mlp_fwd16<false, 0>;
+    case 12:
+      switch (v >> 4) {       // bit4 cross-layer prefetch; bits 5-6 timing experiments
+        case 1: return k_mlp_fwd16<true, 1>;
+        case 2: return k_mlp_fwd16<true, 2>;
+        case 4: return k_mlp_fwd16<true, 4>;
+        default: return k_mlp_fwd16<true, 0>;
+      }
     default: return k_mlp_fwd<0>;
   }
 }
@@ -50,8 +58,12 @@ using JacKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, 
 static JacKernel jac_kernel() {
   const char* e = getenv("DSR_JAC_VARIANT");
   const int v = e ? atoi(e) : 12;
-  if (v == 12) return k_mlp_jac16<true>;
-  if (v == 8) return k_mlp_jac16<false>;
+  switch (v) {
+    case 8: return k_mlp_jac16<false, false>;
+    case 12: return k_mlp_jac16<true, false>;
+    case 24: return k_mlp_jac16<false, true>;
+    case 28: return k_mlp_jac16<true, true>;
+  }
   return k_mlp_jac;
 }
 static int fwd_variant() {
@@ -98,7 +110,9 @@ struct dsr_batch {
   dsr_object_out* out = nullptr;
   float *tr_H = nullptr, *tr_v = nullptr;
   int* tr_i = nullptr;
-  std::vector<hipEvent_t> ev;   // [iters][4] fwd0 fwd1 jac0 jac1 + begin/end
+  int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
+  std::vector<int> passes;      // render-pass rank boundaries, last = M
+  std::vector<hipEvent_t> ev;   // begin, end, then per iteration: fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
 };
 
@@ -374,6 +388,26 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // ------------------------------------------------------------------------------------
 // batches
 // ------------------------------------------------------------------------------------
+// Render-pass schedule of the early ray termination (k_sample_pass): in-ball rank
+// boundaries, DSR_RENDER_PASSES="8,12,16,20,24,32" style (ascending, each < M); one pass
+// [0, M) when empty ("0" disables termination).
+static std::vector<int> render_passes(int M) {
+  const char* e = getenv("DSR_RENDER_PASSES");
+  std::string spec = e ? e : "8,12,16,20,24,32";
+  std::vector<int> r{0};
+  size_t p = 0;
+  while (p < spec.size()) {
+    const size_t q = spec.find(',', p);
+    const int v = atoi(spec.substr(p, q == std::string::npos ? std::string::npos : q - p).c_str());
+    if (v > r.back() && v < M) r.push_back(v);
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  r.push_back(M);
+  return r;
+}
+static size_t ev_per_iter(const dsr_batch* b) { return 2 * (b->passes.size() - 1) + 2; }
+
 static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
   if (bytes == 0) bytes = 256;
   if (hipMalloc(p, bytes) != hipSuccess) return fail(b->ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
@@ -465,6 +499,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->cand, sizeof(float4) * (size_t)cand_off);
   ALLOC(b->kpts, sizeof(float4) * (size_t)cand_off);
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
+  ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->kres, sizeof(float) * (size_t)cand_off);
   ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
   ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
@@ -473,7 +508,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->nt_f, sizeof(int));
   ALLOC(b->nt_j, sizeof(int));
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
-  ALLOC(b->counts, sizeof(int) * 2 * (size_t)std::max(1, b->iters) * n_obj);
+  ALLOC(b->counts, sizeof(int) * 3 * (size_t)std::max(1, b->iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
   if (trace) {
     const size_t it = std::max(1, b->iters);
@@ -500,7 +535,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     hipMemset(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj);
     hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
   }
-  b->ev.resize((size_t)std::max(1, b->iters) * 4 + 2);
+  b->passes = render_passes(M);
+  b->ev.resize((size_t)std::max(1, b->iters) * ev_per_iter(b) + 2);
   for (auto& e : b->ev)
     if (hipEventCreate(&e) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
   *out = b;
@@ -524,27 +560,32 @@ int dsr_batch_run(dsr_batch* b) {
   const int cb = (n + 63) / 64;
   const FwdKernel fwdk = fwd_kernel(fwd_variant());
   const JacKernel jack = jac_kernel();
+  const int np = (int)b->passes.size() - 1;
+  const size_t epi = ev_per_iter(b);
   DSR_CHECK(ctx, hipEventRecord(b->ev[0], s));
   hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
   for (int it = 0; it < b->iters; ++it) {
     hipLaunchKernelGGL(k_iter_begin, dim3(n), dim3(512), 0, s, n, b->desc, b->st, b->zbuf, D, P,
                        b->bias0f, b->bias4f, b->dobs);
-    hipLaunchKernelGGL(k_sample, dim3(n), dim3(SAMPLE_THREADS), 0, s, n, b->desc, b->st, b->rays, b->M,
-                       b->cand, b->dense);
-    hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_f, b->nt_f);
-    DSR_CHECK(ctx, hipMemsetAsync(ctx->sync_ctr, 0, 8 * 32 * sizeof(unsigned), s));
-    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 0], s));
-    hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
-                       b->bias0f, b->bias4f, b->dense, ctx->sync_ctr);
-    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 1], s));
+    hipEvent_t* ev = b->ev.data() + 2 + it * epi;
+    for (int pz = 0; pz < np; ++pz) {            // render passes with early ray termination
+      hipLaunchKernelGGL(k_sample_pass, dim3(n), dim3(SAMPLE_THREADS), 0, s, n, b->desc, b->st, b->rays, b->M,
+                         b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
+      hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_f, b->nt_f);
+      DSR_CHECK(ctx, hipMemsetAsync(ctx->sync_ctr, 0, 8 * 32 * sizeof(unsigned), s));
+      DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
+      hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
+                         b->bias0f, b->bias4f, b->dense, ctx->sync_ctr, ErtArgs{b->dead, b->M, -P.cut_off});
+      DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
+    }
     hipLaunchKernelGGL(k_render, dim3(n), dim3(RENDER_THREADS), 0, s, n, b->desc, b->st, b->rays, b->dobs, P,
                        b->dense, b->kpts, b->kres);
     hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_j, b->nt_j);
-    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 2], s));
+    DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
     hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
                        b->pts, b->kpts, b->kres, b->bias0f, b->bias4f, P, b->slots,
                        (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
-    DSR_CHECK(ctx, hipEventRecord(b->ev[2 + it * 4 + 3], s));
+    DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
     hipLaunchKernelGGL(k_count, dim3(cb), dim3(64), 0, s, n, b->desc, b->st, it, b->counts);
     hipLaunchKernelGGL(k_solve, dim3(n), dim3(SOLVE_THREADS), 0, s, n, b->desc, b->st, b->zbuf, P, b->slots,
                        b->tr_H, b->tr_v, b->tr_i);
@@ -579,21 +620,29 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
   std::memset(st, 0, sizeof(*st));
   float ms = 0.f;
+  const int np = (int)b->passes.size() - 1;
+  const size_t epi = ev_per_iter(b);
   for (int it = 0; it < b->iters; ++it) {
-    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[2 + it * 4 + 0], b->ev[2 + it * 4 + 1]));
-    st->fwd_ms += ms;
-    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[2 + it * 4 + 2], b->ev[2 + it * 4 + 3]));
+    const hipEvent_t* ev = b->ev.data() + 2 + it * epi;
+    for (int pz = 0; pz < np; ++pz) {
+      DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * pz], ev[2 * pz + 1]));
+      st->fwd_ms += ms;
+    }
+    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * np], ev[2 * np + 1]));
     st->jac_ms += ms;
   }
   DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
   st->total_ms = ms;
-  st->fwd_launches = st->jac_launches = b->iters;
-  std::vector<int> c((size_t)2 * std::max(1, b->iters) * b->n_obj);
+  st->fwd_launches = b->iters * np;
+  st->jac_launches = b->iters;
+  std::vector<int> c((size_t)3 * std::max(1, b->iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < b->iters; ++it)
     for (int o = 0; o < b->n_obj; ++o) {
-      st->fwd_points += c[((size_t)it * b->n_obj + o) * 2 + 0];
-      st->jac_points += c[((size_t)it * b->n_obj + o) * 2 + 1];
+      const int* e = c.data() + ((size_t)it * b->n_obj + o) * 3;
+      st->fwd_points += e[0];
+      st->jac_points += e[1];
+      st->inball_points += e[2];
     }
   return 0;
 }
@@ -705,7 +754,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   } else {
     hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
-                       (unsigned*)nullptr);
+                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f});
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     cleanup();

@@ -77,11 +77,21 @@ struct ObjState {
   int iters_done;
   int n_valid, k;        // this iteration's counts
   int n_sdf_tiles, n_ren_tiles, slot_ren;   // this iteration's jac tiles
-  int pad[3];
+  int n_emit;            // ray samples emitted by the current render pass (fwd tiles)
+  int n_eval;            // ray samples decoded this iteration (sum over passes)
+  int pad;
 };
 
 struct Tile {
   int obj, term, start, count;   // term: 0 = sdf (surface points), 1 = render (K list)
+};
+
+// Early ray termination (k_sample_pass): the fwd kernels flag a ray dead once one of its
+// samples decodes to sdf <= -cut_off (occupancy exactly 1, transmittance exactly 0 after it).
+struct ErtArgs {
+  int* dead;             // [sum n_rays] (nullptr: no flagging, e.g. dsr_sdf_eval)
+  int M;                 // samples per ray (grid index = ray * M + j)
+  float nth;             // -cut_off
 };
 
 struct GNParams {

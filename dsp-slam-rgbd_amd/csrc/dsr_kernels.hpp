@@ -1,13 +1,15 @@
 // dsr_kernels.hpp — the device-resident Gauss-Newton iteration of
 // Optimizer.reconstruct_object (reconstruct/optimizer.py:90-205) for a batch of
-// independent objects.  One iteration = 8 launches, none of which needs the host:
+// independent objects.  One iteration = 6 + 3 x (render passes) launches, none of which
+// needs the host:
 //
 //   k_iter_begin   optimizer.py:122-128  t_cam_obj, scale, linspace depths, bg depth,
 //                                        + code folded into lin0 / lin4 biases
-//   k_sample       loss.py:71-88         ray samples -> object frame -> |x|<1 ->
-//                                        ordered compaction (== torch.where order)
-//   k_tiles_fwd    —                     64-point tiles over every object's N_valid
-//   k_mlp_fwd      loss.py:91-92         decode_sdf on all in-ball samples (MFMA)
+//   per render pass (early ray termination, exact — see k_sample_pass):
+//   k_sample_pass  loss.py:71-88         ray samples -> object frame -> |x|<1 ->
+//                                        (ray, depth)-ordered compaction of live rays
+//   k_tiles_fwd    —                     64-point tiles over the pass's samples
+//   k_mlp_fwd      loss.py:91-92         decode_sdf (MFMA), flags terminated rays
 //   k_render       loss.py:97-150        occupancy, transmittance cumprod, rendered
 //                                        depth, de_do, K-compaction, residual clamp
 //   k_tiles_jac    —                     tiles over N surface pts + K render pts
@@ -225,6 +227,7 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
     S.bg_depth = 1.1f * dmax;                                  // :128
     S.n_valid = 0;
     S.k = 0;
+    S.n_emit = S.n_eval = 0;
   }
   __syncthreads();
   const ObjDesc d = desc[o];
@@ -233,7 +236,7 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
 }
 
 // ------------------------------------------------------------------------------------
-// k_sample: ray samples -> object frame -> |x| < 1 -> ordered compaction
+// ray samples -> object frame -> |x| < 1 (loss.py:71-82)
 // ------------------------------------------------------------------------------------
 constexpr int SAMPLE_THREADS = 1024;
 
@@ -244,53 +247,105 @@ __device__ __forceinline__ float3 ray_sample(const float* __restrict__ rays, con
   return xform(S.T, cx, cy, cz);
 }
 
-__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample(int n_obj, const ObjDesc* __restrict__ desc,
-                                                           ObjState* st, const float* __restrict__ rays_all,
-                                                           int M, float4* __restrict__ cand,
-                                                           float* __restrict__ dense) {
+// ------------------------------------------------------------------------------------
+// k_sample_pass: the ray samples of loss.py:71-82, emitted in render passes with early
+// ray termination.  Pass [ra, rb) emits, for every ray not yet flagged dead, its
+// in-ball samples of in-ball rank ra..rb-1 (rank = position among the ray's in-ball
+// samples, depth order).  A ray is flagged dead by the fwd kernel when one of its samples
+// decodes to sdf <= -th: its occupancy is then exactly 1 (0.5 - (-th)/(2 th), loss_utils.py
+// :46-47), the cumulative transmittance exactly 0 from there on (loss.py:111), so every
+// later sample of the ray enters d_u, var_u and de_do (loss.py:112-132) multiplied by an
+// exact zero, and its de_do = 0 fails the 1e-2 filter (:135): decoding it cannot change
+// any output, and k_render sees it only behind T == 0.  Results are bit-identical to
+// decoding every in-ball sample; the first pass also marks the out-of-ball samples (NaN)
+// and counts n_valid (loss.py:82-88) over ALL in-ball samples.
+// One thread per ray, one workgroup per object, (ray, depth)-ordered output.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
+                                                                ObjState* st, const float* __restrict__ rays_all,
+                                                                int M, int ra, int rb, float4* __restrict__ cand,
+                                                                float* __restrict__ dense, int* __restrict__ dead) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
   const ObjDesc d = desc[o];
   const float* rays = rays_all + (size_t)d.ray_off * 3;
-  const int total = d.n_rays * M;
+  const bool first = ra == 0;
   __shared__ int wsum[SAMPLE_THREADS / 64];
-  __shared__ int base_s;
+  __shared__ int wnin[SAMPLE_THREADS / 64];
+  __shared__ int base_s, nin_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) base_s = 0;
+  if (tid == 0) { base_s = 0; nin_s = 0; }
   __syncthreads();
-  for (int c0 = 0; c0 < total; c0 += SAMPLE_THREADS) {
-    const int c = c0 + tid;
-    bool valid = false;
-    float3 x = make_float3(0.f, 0.f, 0.f);
-    if (c < total) {
-      const int ray = c / M, j = c - (c / M) * M;
-      x = ray_sample(rays, S, ray, j);
-      const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
-      valid = nrm < 1.0f;                                              // loss.py:82
-      if (!valid) dense[d.cand_off + c] = __builtin_nanf("");
+  for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
+    const int ray = r0 + tid;
+    int cnt = 0, nin = 0;
+    bool alive = false;
+    if (ray < d.n_rays) {
+      if (first) dead[d.ray_off + ray] = 0;
+      alive = first || dead[d.ray_off + ray] == 0;
+      if (alive) {
+        int rank = 0;
+        for (int j = 0; j < M; ++j) {
+          const float3 x = ray_sample(rays, S, ray, j);
+          const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+          if (!(nrm < 1.0f)) {                                             // loss.py:82
+            if (first) dense[d.cand_off + ray * M + j] = __builtin_nanf("");
+            continue;
+          }
+          if (rank >= ra && rank < rb) ++cnt;
+          ++rank;
+          if (!first && rank >= rb) break;
+        }
+        nin = rank;
+      }
     }
-    const uint64_t bal = __ballot(valid);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[wv] = __popcll(bal);
+    const int inc = wave_incl_scan(cnt, lane);
+    int nin_w = nin;
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) nin_w += __shfl_xor(nin_w, k);
+    if (lane == 63) wsum[wv] = inc;
+    if (lane == 0) wnin[wv] = nin_w;
     __syncthreads();
-    int off = base_s;
+    int off = base_s + inc - cnt;
     for (int k = 0; k < wv; ++k) off += wsum[k];
-    if (valid)
-      cand[d.cand_off + off + before] = make_float4(x.x, x.y, x.z, __int_as_float(c));
+    if (cnt > 0) {
+      int rank = 0;
+      for (int j = 0; j < M && rank < rb; ++j) {
+        const float3 x = ray_sample(rays, S, ray, j);
+        const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
+        if (!(nrm < 1.0f)) continue;
+        if (rank >= ra) cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
+        ++rank;
+      }
+    }
     __syncthreads();
     if (tid == 0) {
-      int t = 0;
-      for (int k = 0; k < SAMPLE_THREADS / 64; ++k) t += wsum[k];
+      int t = 0, u = 0;
+      for (int k = 0; k < SAMPLE_THREADS / 64; ++k) { t += wsum[k]; u += wnin[k]; }
       base_s += t;
+      nin_s += u;
     }
     __syncthreads();
   }
   if (tid == 0) {
-    S.n_valid = base_s;
-    if (base_s < 10) {                        // loss.py:86-88 -> optimizer.py:144-145
-      S.status = ST_FAIL;
-      S.fail_reason = DSR_FAIL_RENDER_FEW;
+    S.n_emit = base_s;
+    S.n_eval += base_s;
+    if (first) {
+      S.n_valid = nin_s;
+      if (nin_s < 10) {                        // loss.py:86-88 -> optimizer.py:144-145
+        S.status = ST_FAIL;
+        S.fail_reason = DSR_FAIL_RENDER_FEW;
+      }
     }
   }
 }
@@ -305,7 +360,7 @@ __global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const O
   __syncthreads();
   for (int o = 0; o < n_obj; ++o) {
     const ObjState& S = st[o];
-    const int n = (S.status == ST_RUNNING) ? S.n_valid : 0;
+    const int n = (S.status == ST_RUNNING) ? S.n_emit : 0;
     const int nt = (n + TILE - 1) / TILE;
     const int b = base_s;
     for (int i = threadIdx.x; i < nt; i += blockDim.x) {
@@ -377,7 +432,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
                                                  const float* __restrict__ bias0f,
                                                  const float* __restrict__ bias4f,
                                                  float* __restrict__ dense,
-                                                 unsigned* __restrict__ sync_ctr) {
+                                                 unsigned* __restrict__ sync_ctr, ErtArgs E) {
   __shared__ FwdShared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -419,6 +474,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
       const float y = tanhf(s + D.b8);
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
       dense[d.cand_off + idx] = y;
+      if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;
     }
     __syncthreads();
   }
@@ -765,7 +821,7 @@ struct Jac16Shared {
   float wmax[NWAVE];
 };
 
-template <bool PRIO>
+template <bool PRIO, bool XP>
 __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
                                                    const ObjDesc* __restrict__ desc,
@@ -784,6 +840,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
   const int nt = *n_tiles;
+  const int T1 = D.Kf[1] / 32;
+  half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
+  if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
@@ -846,8 +905,13 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 32;
-      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
-                           sm.Hh, sm.Hl, acc, lane);
+      if constexpr (XP) {
+        const int Tn = D.Kf[l + 1] / 32;
+        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                               wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
+      } else {
+        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
+      }
       const float usc = ldexpf(1.f, -(D.sw[l] + sa));
       const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
       float m = 0.f;
@@ -876,8 +940,13 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     // ---- lin7 + lin8 dot + tanh
     {
       const int T = D.Kf[7] / 32;
-      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T,
-                           sm.Hh, sm.Hl, acc, lane);
+      if constexpr (XP) {
+        const int Tn = D.Kb[7] / 32;
+        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                               wfrag(D.Wbh_raw[7], w, Tn), Tn);
+      } else {
+        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
+      }
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -922,8 +991,14 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll 1
     for (int l = 7; l >= 1; --l) {
       const int T = D.Kb[l] / 32;
-      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wbh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T,
-                           sm.Hh, sm.Hl, acc, lane);
+      if constexpr (XP) {       // next: lin_{l-1}^T, or lin1 of the next tile after lin1^T
+        const _Float16* Wn = (l > 1) ? D.Wbh_raw[l - 1] : D.Wh_raw[1];
+        const int Tn = (l > 1) ? D.Kb[l - 1] / 32 : T1;
+        gemm16_tile_x<PRIO, 4>(wfrag(D.Wbh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                               wfrag(Wn, w, Tn), Tn);
+      } else {
+        gemm16_tile<PRIO, 4>(wfrag(D.Wbh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
+      }
       const float usc = ldexpf(1.f, -(D.swb[l] + sa));
       float m = 0.f;
       const uint64_t mask = mk[l - 1];
@@ -1216,8 +1291,10 @@ __global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjSt
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= n_obj) return;
   const ObjState& S = st[o];
-  counts[((size_t)it * n_obj + o) * 2 + 0] = S.n_valid;
-  counts[((size_t)it * n_obj + o) * 2 + 1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
+  int* c = counts + ((size_t)it * n_obj + o) * 3;
+  c[0] = S.n_eval;
+  c[1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
+  c[2] = S.n_valid;
 }
 
 __global__ void k_finalize(int n_obj, const ObjState* __restrict__ st, const float* __restrict__ zbuf,

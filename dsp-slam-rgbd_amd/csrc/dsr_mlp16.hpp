@@ -60,7 +60,74 @@ __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&
   if (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
+// This wave's slice (row blocks 4w..4w+3) of a packed split-fp16 weight matrix with T k-steps.
+__device__ __forceinline__ const half8* wfrag(const _Float16* W, int w, int T) {
+  return reinterpret_cast<const half8*>(W) + (size_t)(4 * w) * T * 2 * 64;
+}
+
+// First-k-step A fragments of a packed weight matrix (the GEMM's prologue load).
+template <int NQ>
+__device__ __forceinline__ void load_a0(const half8* __restrict__ A, int T, half8 (&ah)[NQ], half8 (&al)[NQ],
+                                        int lane) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    ah[q] = A[((q * T) * 2 + 0) * 64 + lane];
+    al[q] = A[((q * T) * 2 + 1) * 64 + lane];
+  }
+}
+
 // acc = A(16*NQ rows of this wave) . H (64 points), K = 32*T.  A: packed [(q*T + t)*2 + piece][lane].
+// On entry ah0/al0 hold A's first-k-step fragments; on exit they hold those of the NEXT
+// weight matrix An (Tn k-steps), so its L2 latency hides behind this GEMM's last step, the
+// epilogue and the barrier instead of stalling the next layer's first MFMA.
+template <bool PRIO, int NQ = 4>
+__device__ __forceinline__ void gemm16_tile_x(const half8* __restrict__ A, int T, const _Float16* Hh,
+                                              const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane,
+                                              half8 (&ah0)[NQ], half8 (&al0)[NQ],
+                                              const half8* __restrict__ An, int Tn) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const _Float16* Bh = Hh + boff;
+  const _Float16* Bl = Hl + boff;
+  half8 ah1[NQ], al1[NQ], bh0[4], bl0[4], bh1[4], bl1[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH);
+    bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH);
+  }
+  for (int t = 0; t < T; t += 2) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      ah1[q] = A[((q * T + t + 1) * 2 + 0) * 64 + lane];
+      al1[q] = A[((q * T + t + 1) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      bh1[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 1));
+      bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
+    }
+    mfma3_step<PRIO, NQ>(ah0, al0, bh0, bl0, acc);
+    if (t + 2 < T) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        ah0[q] = A[((q * T + t + 2) * 2 + 0) * 64 + lane];
+        al0[q] = A[((q * T + t + 2) * 2 + 1) * 64 + lane];
+      }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 2));
+        bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 2));
+      }
+    } else {
+      load_a0<NQ>(An, Tn, ah0, al0, lane);
+    }
+    mfma3_step<PRIO, NQ>(ah1, al1, bh1, bl1, acc);
+  }
+}
+
 template <bool PRIO, int NQ = 4>
 __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
                                             const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane) {
@@ -72,11 +139,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
   half8 ah0[NQ], al0[NQ], ah1[NQ], al1[NQ], bh0[4], bl0[4], bh1[4], bl1[4];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    ah0[q] = A[((q * T) * 2 + 0) * 64 + lane];
-    al0[q] = A[((q * T) * 2 + 1) * 64 + lane];
-  }
+  load_a0<NQ>(A, T, ah0, al0, lane);
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
     bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH);
@@ -197,19 +260,27 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
   return s;
 }
 
-template <bool PRIO>
+// X: bit0 cross-layer A prefetch; bits 1-2 = timing experiments only (results invalid):
+// 2 = epilogue reduced to one fp16 store, 4 = no epilogue (GEMMs + barriers only).
+template <bool PRIO, int X>
 __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
                                                    const ObjDesc* __restrict__ desc,
                                                    const float4* __restrict__ cand,
                                                    const float* __restrict__ bias0f,
                                                    const float* __restrict__ bias4f,
-                                                   float* __restrict__ dense, unsigned* __restrict__) {
+                                                   float* __restrict__ dense, unsigned* __restrict__,
+                                                   ErtArgs E) {
   __shared__ Fwd16Shared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c = lane & 15;
   const int nt = *n_tiles;
+  constexpr bool XP = (X & 1) != 0;
+  constexpr int EXPM = X & 6;
+  const int T1 = D.Kf[1] / 32;
+  half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
+  if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
@@ -257,13 +328,36 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     floatx4 acc[4][4];
     for (int l = 1; l <= 6; ++l) {
       const int T = D.Kf[l] / 32;
-      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[l]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
-      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
+      if constexpr (XP) {
+        const int Tn = D.Kf[l + 1] / 32;
+        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                               wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
+      } else {
+        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
+      }
+      if constexpr (EXPM == 0) {
+        sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
+      } else if constexpr (EXPM == 2) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            half4 hh;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hh[r] = (_Float16)accr(acc[q][cb], r);
+            *reinterpret_cast<half4*>(sm.Hh + (16 * cb + c) * PH + 64 * w + 16 * q + 4 * g) = hh;
+          }
+      }
       __syncthreads();
     }
     {
       const int T = D.Kf[7] / 32;
-      gemm16_tile<PRIO, 4>(reinterpret_cast<const half8*>(D.Wh_raw[7]) + (size_t)(4 * w) * T * 2 * 64, T, sm.Hh, sm.Hl, acc, lane);
+      if constexpr (XP)      // prefetch lin1 of the next tile (same weights every tile)
+        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                               wfrag(D.Wh_raw[1], w, T1), T1);
+      else
+        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -286,6 +380,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       if (px != px || py != py || pz != pz || zprobe != zprobe) y = __builtin_nanf("");
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
       dense[d.cand_off + idx] = y;
+      if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
     }
     __syncthreads();
   }

@@ -62,10 +62,13 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
+ABI_VERSION = 2          # include/dsr.h DSR_ABI_VERSION
+
+
 class Stats(C.Structure):
     _fields_ = [("fwd_ms", C.c_double), ("jac_ms", C.c_double), ("total_ms", C.c_double),
                 ("fwd_points", C.c_int64), ("jac_points", C.c_int64),
-                ("fwd_launches", C.c_int), ("jac_launches", C.c_int)]
+                ("fwd_launches", C.c_int), ("jac_launches", C.c_int), ("inball_points", C.c_int64)]
 
 
 #: every function declared in include/dsr.h, with its ctypes signature
@@ -116,7 +119,7 @@ def load_library(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dsr_abi_version() != 1:
+        if lib.dsr_abi_version() != ABI_VERSION:
             raise DsrError("libdsr ABI version mismatch")
         if path is None:
             _lib = lib

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 1
+#define DSR_ABI_VERSION 2
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -118,9 +118,11 @@ typedef struct {
   double fwd_ms;                  /* summed device time of the ray-sample decoder kernel */
   double jac_ms;                  /* summed device time of the fwd+Jacobian kernel */
   double total_ms;                /* wall (device events) of the last run */
-  int64_t fwd_points;             /* sum over iterations/objects of N_valid */
+  int64_t fwd_points;             /* ray samples decoded (early ray termination skips the
+                                     samples behind a ray's first sdf <= -cut_off) */
   int64_t jac_points;             /* sum of (N + K) */
-  int fwd_launches, jac_launches;
+  int fwd_launches, jac_launches; /* fwd: one per render pass per iteration */
+  int64_t inball_points;          /* sum over iterations/objects of N_valid (in-ball samples) */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */

@@ -342,3 +342,51 @@ def test_nan_propagation(gpu_decoder):
     z2 = z.copy()
     z2[3] = np.nan
     assert np.isnan(sdf_eval(gpu_decoder, z2, x)).all()
+
+
+def test_early_ray_termination_matches_full_decode(gpu_decoder, monkeypatch):
+    """Render passes with early ray termination (k_sample_pass) vs decoding every in-ball
+    sample (DSR_RENDER_PASSES=0): same N_valid and K, same step up to the per-tile
+    split-fp16 scale (tiles are composed differently), and far fewer samples decoded.
+    Exactness of the skip itself: tests/test_ert_cpu.py (bitwise, on the oracle)."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    f = golden("f4_traj_kitti0.npz")
+    one = dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=1))
+    opt = _opt(gpu_decoder, one, "KITTI")
+    n_it = int(f["n_iters_run"])
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
+            for e in range(n_it)]
+    out = {}
+    for spec in ("0", "8,12,16,20,24,32", "4,5,6,7,8,9,10,11,12,14,16,20,24,28,32,40"):
+        monkeypatch.setenv("DSR_RENDER_PASSES", spec)
+        out[spec] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    full_res, full_tr = out["0"]
+    for spec in list(out)[1:]:
+        res, tr = out[spec]
+        for e in range(n_it):
+            assert res[e]["is_good"] == full_res[e]["is_good"]
+            assert int(tr[e]["n_valid"][0]) == int(full_tr[e]["n_valid"][0])
+            assert int(tr[e]["k"][0]) == int(full_tr[e]["k"][0]), (spec, e)
+            assert abs(tr[e]["loss"][0] - full_tr[e]["loss"][0]) <= 1e-5 * abs(full_tr[e]["loss"][0])
+            assert rel(tr[e]["H"][0], full_tr[e]["H"][0]) <= 1e-4
+            assert step_err(tr[e]["dx"][0], full_tr[e]["dx"][0], full_tr[e]["H"][0]) <= 1e-3
+
+    params = L.optim_params(one)
+    pts = {}
+    for spec in ("0", "8,12,16,20,24,32"):
+        monkeypatch.setenv("DSR_RENDER_PASSES", spec)
+        h, keep = bench.make_batch(gpu_decoder, params, 8, 1000)
+        lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+        try:
+            ctx.check(lib.dsr_batch_run(h), "run")
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+            pts[spec] = (st.fwd_points, st.fwd_launches)
+        finally:
+            lib.dsr_batch_destroy(h)
+    assert pts["0"][1] == 1 and pts["8,12,16,20,24,32"][1] == 7
+    assert pts["8,12,16,20,24,32"][0] < 0.8 * pts["0"][0], pts
