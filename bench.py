@@ -38,6 +38,9 @@ FP16_MFMA_PEAK_TF = 2500.0          # dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PRODUCTS = 3                  # 3xFP16: hi*hi + hi*lo + lo*hi per fp32 product
 
 
+LAST_CREATE_S = None
+
+
 def make_batch(dec, opt_params, n_obj, base_seed):
     from reconstruct import _libdsr as L
 
@@ -56,8 +59,11 @@ def make_batch(dec, opt_params, n_obj, base_seed):
         ins[i] = r
     ctx = dec.ctx
     h = C.c_void_p()
+    global LAST_CREATE_S
+    t0 = time.perf_counter()
     ctx.check(ctx.lib.dsr_batch_create(ctx.handle, dec.handle, C.byref(opt_params), n_obj, ins,
                                        C.byref(h)), "dsr_batch_create")
+    LAST_CREATE_S = time.perf_counter() - t0          # host -> HBM upload of the inputs (PCIe)
     return h, keep
 
 
@@ -249,6 +255,9 @@ def main():
             "job_tflops": round(job_tf, 3),
             "jac_kernel_tflops": round(jac_flop / (jac_ms * 1e-3) / 1e12, 3) if jac_ms > 0 else 0.0,
             "good_fraction": n_good / float(n_obj * args.steps),
+            # inputs handed over in host memory: dsr_batch_create's upload added to one step
+            "host_inclusive_value": n_obj * world / (elapsed / args.steps + LAST_CREATE_S),
+            "batch_create_ms": LAST_CREATE_S * 1e3,
             "cpu_baseline": None,
         }
         tr = pmc_traffic()
