@@ -21,17 +21,19 @@
 
 using namespace dsr;
 
+constexpr int MAX_GROUPS = 4;       // = GPU_MAX_HW_QUEUES on the box
+
 struct dsr_ctx {
   int device = 0;
   int n_cu = 256;
   hipStream_t stream = nullptr;
-  unsigned* sync_ctr = nullptr;    // 8 groups x 32 uints (128-B apart) for the fwd soft sync
+  hipStream_t gstream[MAX_GROUPS] = {};   // [0] = stream; [1..] object-group streams
   std::string err;
 };
 
 // Forward-kernel variant (DSR_FWD_VARIANT, bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
-// bit3 split-fp16, bit4 cross-layer A prefetch (split-fp16 only); 12+32 / 12+64 are timing
-// experiments with a reduced / no epilogue (invalid results))
+// bit3 split-fp16, bit4 cross-layer A prefetch (split-fp16 only); 12 + 16*{2,4,8,16,24} are
+// timing experiments with invalid results: reduced / no epilogue, one MFMA product, no A streaming)
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                            const float*, float*, unsigned*, ErtArgs);
 static FwdKernel fwd_kernel(int v) {
@@ -47,6 +49,9 @@ static FwdKernel fwd_kernel(int v) {
         case 1: return k_mlp_fwd16<true, 1>;
         case 2: return k_mlp_fwd16<true, 2>;
         case 4: return k_mlp_fwd16<true, 4>;
+        case 8: return k_mlp_fwd16<true, 8>;       // 1 product
+        case 16: return k_mlp_fwd16<true, 16>;     // no A streaming
+        case 24: return k_mlp_fwd16<true, 24>;     // both
         default: return k_mlp_fwd16<true, 0>;
       }
     default: return k_mlp_fwd<0>;
@@ -103,8 +108,18 @@ struct dsr_batch {
   float4 *cand = nullptr, *kpts = nullptr;
   float *dense = nullptr, *kres = nullptr;
   float *bias0f = nullptr, *bias4f = nullptr;
-  Tile *tiles_f = nullptr, *tiles_j = nullptr;
-  int *nt_f = nullptr, *nt_j = nullptr;
+  // Object groups: contiguous object ranges whose GN iterations run on their own streams,
+  // so one group's latency-bound kernels and kernel tails overlap the other's decoder
+  // kernels (objects never interact; every group owns its tile tables and counters).
+  struct Group {
+    int o0 = 0, n = 0;
+    Tile *tiles_f = nullptr, *tiles_j = nullptr;
+    int *nt_f = nullptr, *nt_j = nullptr;
+    unsigned* sync = nullptr;
+  };
+  std::vector<Group> groups;
+  hipEvent_t fork_ev = nullptr;
+  std::vector<hipEvent_t> join_ev;
   float* slots = nullptr;
   int* counts = nullptr;
   dsr_object_out* out = nullptr;
@@ -112,7 +127,7 @@ struct dsr_batch {
   int* tr_i = nullptr;
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
   std::vector<int> passes;      // render-pass rank boundaries, last = M
-  std::vector<hipEvent_t> ev;   // begin, end, then per iteration: fwd0/fwd1 per pass, jac0, jac1
+  std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
 };
 
@@ -156,11 +171,13 @@ int dsr_ctx_create(int device, dsr_ctx** out) {
     delete c;
     return -1;
   }
-  if (hipMalloc(&c->sync_ctr, 8 * 32 * sizeof(unsigned)) != hipSuccess) {
-    hipStreamDestroy(c->stream);
-    delete c;
-    return -1;
-  }
+  c->gstream[0] = c->stream;
+  for (int g = 1; g < MAX_GROUPS; ++g)
+    if (hipStreamCreateWithFlags(&c->gstream[g], hipStreamNonBlocking) != hipSuccess) {
+      for (int k = 0; k < g; ++k) hipStreamDestroy(c->gstream[k]);
+      delete c;
+      return -1;
+    }
   *out = c;
   return 0;
 }
@@ -168,8 +185,9 @@ int dsr_ctx_create(int device, dsr_ctx** out) {
 int dsr_ctx_destroy(dsr_ctx* ctx) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
+  for (int g = 1; g < MAX_GROUPS; ++g)
+    if (ctx->gstream[g]) hipStreamDestroy(ctx->gstream[g]);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
-  if (ctx->sync_ctr) hipFree(ctx->sync_ctr);
   delete ctx;
   return 0;
 }
@@ -428,6 +446,8 @@ int dsr_batch_destroy(dsr_batch* b) {
   if (!b) return 0;
   hipSetDevice(b->ctx->device);
   for (auto& e : b->ev) hipEventDestroy(e);
+  for (auto& e : b->join_ev) hipEventDestroy(e);
+  if (b->fork_ev) hipEventDestroy(b->fork_ev);
   for (void* p : b->allocs) hipFree(p);
   delete b;
   return 0;
@@ -452,7 +472,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   b->M = p->num_depth_samples;
   const int M = b->M;
   std::vector<float> hpts, hrays, hdobs, hz((size_t)n_obj * CODE, 0.f), ht((size_t)n_obj * 16);
-  std::vector<int> hoc(n_obj);
+  std::vector<int> hoc(n_obj), ftile_o(n_obj), jtile_o(n_obj);
   int pts_off = 0, ray_off = 0, cand_off = 0, slot_off = 0, ftiles = 0;
   for (int o = 0; o < n_obj; ++o) {
     const dsr_object_in& x = in[o];
@@ -477,8 +497,22 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     pts_off += x.n_pts;
     ray_off += x.n_rays;
     cand_off += cap;
-    ftiles += (cap + TILE - 1) / TILE;
-    slot_off += (x.n_pts + TILE - 1) / TILE + (cap + TILE - 1) / TILE;
+    ftile_o[o] = (cap + TILE - 1) / TILE;
+    jtile_o[o] = (x.n_pts + TILE - 1) / TILE + (cap + TILE - 1) / TILE;
+    ftiles += ftile_o[o];
+    slot_off += jtile_o[o];
+  }
+  {
+    const char* e = getenv("DSR_STREAMS");
+    int G = e ? atoi(e) : 2;
+    G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
+    if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
+    for (int g = 0; g < G; ++g) {
+      dsr_batch::Group gr;
+      gr.o0 = (int)((long)n_obj * g / G);
+      gr.n = (int)((long)n_obj * (g + 1) / G) - gr.o0;
+      b->groups.push_back(gr);
+    }
   }
   b->cand_total = cand_off;
   b->slot_total = slot_off;
@@ -503,10 +537,15 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->kres, sizeof(float) * (size_t)cand_off);
   ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
   ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
-  ALLOC(b->tiles_f, sizeof(Tile) * (size_t)ftiles);
-  ALLOC(b->tiles_j, sizeof(Tile) * (size_t)slot_off);
-  ALLOC(b->nt_f, sizeof(int));
-  ALLOC(b->nt_j, sizeof(int));
+  for (auto& gr : b->groups) {
+    size_t ft = 0, jt = 0;
+    for (int o = gr.o0; o < gr.o0 + gr.n; ++o) { ft += ftile_o[o]; jt += jtile_o[o]; }
+    ALLOC(gr.tiles_f, sizeof(Tile) * std::max<size_t>(1, ft));
+    ALLOC(gr.tiles_j, sizeof(Tile) * std::max<size_t>(1, jt));
+    ALLOC(gr.nt_f, sizeof(int));
+    ALLOC(gr.nt_j, sizeof(int));
+    ALLOC(gr.sync, 8 * 32 * sizeof(unsigned));
+  }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
   ALLOC(b->counts, sizeof(int) * 3 * (size_t)std::max(1, b->iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
@@ -536,9 +575,19 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
   }
   b->passes = render_passes(M);
-  b->ev.resize((size_t)std::max(1, b->iters) * ev_per_iter(b) + 2);
+  b->ev.resize((size_t)std::max(1, b->iters) * b->groups.size() * ev_per_iter(b) + 2);
+  b->join_ev.resize(b->groups.size());
   for (auto& e : b->ev)
     if (hipEventCreate(&e) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
+  for (auto& e : b->join_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      dsr_batch_destroy(b);
+      return fail(ctx, "hipEventCreate failed");
+    }
+  if (hipEventCreateWithFlags(&b->fork_ev, hipEventDisableTiming) != hipSuccess) {
+    dsr_batch_destroy(b);
+    return fail(ctx, "hipEventCreate failed");
+  }
   *out = b;
   return 0;
 }
@@ -552,47 +601,67 @@ int dsr_batch_run(dsr_batch* b) {
   if (!b) return -2;
   dsr_ctx* ctx = b->ctx;
   hipSetDevice(ctx->device);
-  hipStream_t s = ctx->stream;
+  hipStream_t s0 = ctx->stream;
   const int n = b->n_obj;
   const DevDecoder& D = b->dec->D;
   const GNParams P = b->P;
   const int grid = ctx->n_cu;
   const int cb = (n + 63) / 64;
-  const FwdKernel fwdk = fwd_kernel(fwd_variant());
+  const int fv = fwd_variant();
+  const FwdKernel fwdk = fwd_kernel(fv);
   const JacKernel jack = jac_kernel();
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
-  DSR_CHECK(ctx, hipEventRecord(b->ev[0], s));
-  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
+  const int G = (int)b->groups.size();
+  DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
+  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s0, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
+  DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
+  for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
   for (int it = 0; it < b->iters; ++it) {
-    hipLaunchKernelGGL(k_iter_begin, dim3(n), dim3(512), 0, s, n, b->desc, b->st, b->zbuf, D, P,
-                       b->bias0f, b->bias4f, b->dobs);
-    hipEvent_t* ev = b->ev.data() + 2 + it * epi;
-    for (int pz = 0; pz < np; ++pz) {            // render passes with early ray termination
-      hipLaunchKernelGGL(k_sample_pass, dim3(n), dim3(SAMPLE_THREADS), 0, s, n, b->desc, b->st, b->rays, b->M,
-                         b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
-      hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_f, b->nt_f);
-      DSR_CHECK(ctx, hipMemsetAsync(ctx->sync_ctr, 0, 8 * 32 * sizeof(unsigned), s));
-      DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
-      hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, b->tiles_f, b->nt_f, b->desc, b->cand,
-                         b->bias0f, b->bias4f, b->dense, ctx->sync_ctr, ErtArgs{b->dead, b->M, -P.cut_off});
-      DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
+    for (int g = 0; g < G; ++g) {             // groups interleaved, one stream each
+      const dsr_batch::Group& gr = b->groups[g];
+      hipStream_t s = ctx->gstream[g];
+      const int ng = gr.n, o0 = gr.o0;
+      const ObjDesc* desc = b->desc + o0;
+      ObjState* st = b->st + o0;
+      float* zbuf = b->zbuf + (size_t)o0 * CODE;
+      float* b0 = b->bias0f + (size_t)o0 * HID;
+      float* b4 = b->bias4f + (size_t)o0 * HID;
+      hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
+      hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
+      for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
+        hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
+                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f);
+        if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
+        DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
+        hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                           b0, b4, b->dense, gr.sync, ErtArgs{b->dead, b->M, -P.cut_off});
+        DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
+      }
+      hipLaunchKernelGGL(k_render, dim3(ng), dim3(RENDER_THREADS), 0, s, ng, desc, st, b->rays, b->dobs, P,
+                         b->dense, b->kpts, b->kres);
+      hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
+      DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
+      hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
+                         b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
+                         (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
+      DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
+      hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
+                         b->counts + (size_t)o0 * 3, n);
+      hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, b->slots,
+                         b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
+                         b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
+                         b->tr_i ? b->tr_i + (size_t)o0 * 2 : nullptr, n);
     }
-    hipLaunchKernelGGL(k_render, dim3(n), dim3(RENDER_THREADS), 0, s, n, b->desc, b->st, b->rays, b->dobs, P,
-                       b->dense, b->kpts, b->kres);
-    hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, n, b->desc, b->st, b->tiles_j, b->nt_j);
-    DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
-    hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, b->tiles_j, b->nt_j, b->desc, b->st,
-                       b->pts, b->kpts, b->kres, b->bias0f, b->bias4f, P, b->slots,
-                       (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
-    DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
-    hipLaunchKernelGGL(k_count, dim3(cb), dim3(64), 0, s, n, b->desc, b->st, it, b->counts);
-    hipLaunchKernelGGL(k_solve, dim3(n), dim3(SOLVE_THREADS), 0, s, n, b->desc, b->st, b->zbuf, P, b->slots,
-                       b->tr_H, b->tr_v, b->tr_i);
   }
-  hipLaunchKernelGGL(k_finalize, dim3(cb), dim3(64), 0, s, n, b->st, b->zbuf, b->out);
+  for (int g = 1; g < G; ++g) {
+    DSR_CHECK(ctx, hipEventRecord(b->join_ev[g], ctx->gstream[g]));
+    DSR_CHECK(ctx, hipStreamWaitEvent(s0, b->join_ev[g], 0));
+  }
+  hipLaunchKernelGGL(k_finalize, dim3(cb), dim3(64), 0, s0, n, b->st, b->zbuf, b->out);
   DSR_CHECK(ctx, hipGetLastError());
-  DSR_CHECK(ctx, hipEventRecord(b->ev[1], s));
+  DSR_CHECK(ctx, hipEventRecord(b->ev[1], s0));
   b->ran = true;
   return 0;
 }
@@ -622,19 +691,21 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   float ms = 0.f;
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
-  for (int it = 0; it < b->iters; ++it) {
-    const hipEvent_t* ev = b->ev.data() + 2 + it * epi;
-    for (int pz = 0; pz < np; ++pz) {
-      DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * pz], ev[2 * pz + 1]));
-      st->fwd_ms += ms;
+  const int G = (int)b->groups.size();
+  for (int it = 0; it < b->iters; ++it)
+    for (int g = 0; g < G; ++g) {
+      const hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
+      for (int pz = 0; pz < np; ++pz) {
+        DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * pz], ev[2 * pz + 1]));
+        st->fwd_ms += ms;
+      }
+      DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * np], ev[2 * np + 1]));
+      st->jac_ms += ms;
     }
-    DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * np], ev[2 * np + 1]));
-    st->jac_ms += ms;
-  }
   DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
   st->total_ms = ms;
-  st->fwd_launches = b->iters * np;
-  st->jac_launches = b->iters;
+  st->fwd_launches = b->iters * np * G;
+  st->jac_launches = b->iters * G;
   std::vector<int> c((size_t)3 * std::max(1, b->iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < b->iters; ++it)

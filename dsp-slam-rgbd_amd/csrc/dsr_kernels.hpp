@@ -481,9 +481,18 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
 }
 
 // ------------------------------------------------------------------------------------
-// k_render: per-ray occupancy scan (loss.py:97-150), one workgroup per object
+// k_render: per-ray occupancy scan (loss.py:97-150), one 512-thread workgroup per object,
+// one thread per ray; the per-ray transmittance row lives in LDS (pitch MAXM+1: the
+// threads of a wave hit 64 different banks), occupancies are re-derived from `dense`.
 // ------------------------------------------------------------------------------------
-constexpr int RENDER_THREADS = 128;
+constexpr int RENDER_THREADS = 512;
+
+__device__ __forceinline__ float occupancy(float s, float nth, float th, float two_th) {
+  // sdf_to_occupancy (loss_utils.py:40-48); NaN marks a sample outside the unit ball
+  // (occ_values initialised to 0, loss.py:97-99)
+  if (s != s) return 0.f;
+  return 0.5f - fminf(fmaxf(s, nth), th) / two_th;
+}
 
 __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjDesc* __restrict__ desc,
                                                            ObjState* st, const float* __restrict__ rays_all,
@@ -500,80 +509,82 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
   const float nth = -th, two_th = 2.0f * th;
   const float do_ds = (float)(-1.0 / (2.0 * (double)th));
   const float* rays = rays_all + (size_t)d.ray_off * 3;
-  __shared__ float occ_s[RENDER_THREADS * (MAXM + 1)];
   __shared__ float T_s[RENDER_THREADS * (MAXM + 1)];
-  __shared__ int cnt_s[RENDER_THREADS];
+  __shared__ float dep_s[MAXM];
+  __shared__ int wsum[RENDER_THREADS / 64];
   __shared__ int base_s;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) base_s = 0;
+  if (tid < M) dep_s[tid] = S.depths[tid];
   __syncthreads();
   const float dmax = S.dmax, delta_d = S.delta_d;
-  float* occ = occ_s + tid * (MAXM + 1);
   float* Tr = T_s + tid * (MAXM + 1);
   for (int r0 = 0; r0 < d.n_rays; r0 += RENDER_THREADS) {
     const int ray = r0 + tid;
-    int cnt = 0;
+    int cnt = 0, jend = 0;
     float du = 0.f, dob = 0.f;
-    uint64_t grad = 0;
+    uint64_t keep = 0;
+    const float* sd = dense + d.cand_off + (size_t)ray * M;
     if (ray < d.n_rays) {
-      const float* sd = dense + d.cand_off + (size_t)ray * M;
-      for (int j = 0; j < M; ++j) {
-        const float s = sd[j];
-        float ov = 0.f;
-        if (!(s != s)) {                              // valid sample (dense holds NaN outside)
-          const float cl = fminf(fmaxf(s, nth), th);
-          ov = 0.5f - cl / two_th;                    // sdf_to_occupancy (loss_utils.py:40-48)
-          if (s > nth && s < th) grad |= 1ull << j;   // loss.py:101
-        }
-        occ[j] = ov;
-      }
       // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
       // probabilities and rendered depth (:112-125).  The 51-term sum is accumulated in
       // fp64 and rounded once: torch's vectorised fp32 sum is within ~1 ulp of exact,
       // a sequential fp32 sum is not (d ~ 15 m, residual d_obs - d_u ~ 1 cm).
+      // Once T == 0 (a sample with occupancy exactly 1) every later term probability,
+      // transmittance and de_do is an exact 0: the scan stops there — the samples behind
+      // were not decoded (early ray termination, k_sample_pass) and cannot matter.
+      uint64_t grad = 0;
       float T = 1.f;
       double dud = 0.0;
-      for (int j = 0; j < M; ++j) {
-        const float tp = occ[j] * T;
-        T = T * (1.f - occ[j]);
+      int j = 0;
+      for (; j < M && T != 0.f; ++j) {
+        const float s = sd[j];
+        const float ov = occupancy(s, nth, th, two_th);
+        if (s > nth && s < th) grad |= 1ull << j;     // loss.py:101
+        const float tp = ov * T;
+        T = T * (1.f - ov);
         Tr[j] = T;
-        dud += (double)(S.depths[j] * tp);
+        dud += (double)(dep_s[j] * tp);
       }
+      jend = j;                                       // Tr[l] = 0 for l >= jend
       dud += (double)((1.1f * dmax) * T);            // background bin o=1, d=1.1*d_max
       du = (float)dud;
       dob = dobs_all[d.ray_off + ray];
       for (uint64_t m = grad; m; m &= m - 1) {
-        const int j = __builtin_ctzll(m);
+        const int jj = __builtin_ctzll(m);
         double sacc = 0.0;
-        for (int l = j; l < M; ++l) sacc += (double)Tr[l];
-        const float dedo = (float)sacc / (1.f - occ[j]);     // :131-132
-        if (dedo > 1e-2f) ++cnt;                      // :135
+        for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
+        const float dedo = (float)sacc / (1.f - occupancy(sd[jj], nth, th, two_th));   // :131-132
+        if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; }                              // :135
       }
     }
-    cnt_s[tid] = cnt;
+    const int inc = wave_incl_scan(cnt, lane);
+    if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    int off = base_s;
-    for (int k = 0; k < tid; ++k) off += cnt_s[k];
+    int off = base_s + inc - cnt;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
     if (cnt > 0) {
       float res = dob - du;                           // :145
       res = res > 0.30f ? 0.30f : res;                // :147-148
       res = res < -0.30f ? -0.30f : res;
-      for (uint64_t m = grad; m; m &= m - 1) {
-        const int j = __builtin_ctzll(m);
+      for (uint64_t m = keep; m; m &= m - 1) {
+        const int jj = __builtin_ctzll(m);
         double sacc = 0.0;
-        for (int l = j; l < M; ++l) sacc += (double)Tr[l];
-        const float dedo = (float)sacc / (1.f - occ[j]);
-        if (dedo > 1e-2f) {
-          const float deds = (dedo * delta_d) * do_ds;  // :142
-          const float3 x = ray_sample(rays, S, ray, j);
-          kpts[d.cand_off + off] = make_float4(x.x, x.y, x.z, deds);
-          kres[d.cand_off + off] = res;
-          ++off;
-        }
+        for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
+        const float dedo = (float)sacc / (1.f - occupancy(sd[jj], nth, th, two_th));
+        const float deds = (dedo * delta_d) * do_ds;    // :142
+        const float3 x = ray_sample(rays, S, ray, jj);
+        kpts[d.cand_off + off] = make_float4(x.x, x.y, x.z, deds);
+        kres[d.cand_off + off] = res;
+        ++off;
       }
     }
     __syncthreads();
-    if (tid == RENDER_THREADS - 1) base_s = off;   // = base + sum of this chunk's counts
+    if (tid == 0) {
+      int t = 0;
+      for (int k = 0; k < RENDER_THREADS / 64; ++k) t += wsum[k];
+      base_s += t;
+    }
     __syncthreads();
   }
   if (tid == 0) S.k = base_s;
@@ -1066,12 +1077,14 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 constexpr int SOLVE_THREADS = 256;
 constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render, T, z
 
+// trace_* hold [iteration][stride objects]; the pointers are pre-offset to this launch's
+// first object (object groups on concurrent streams, dsr_batch_run).
 __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDesc* __restrict__ desc,
                                                          ObjState* st, float* __restrict__ zbuf,
                                                          GNParams P, const float* __restrict__ slots,
                                                          float* __restrict__ trace_H,
                                                          float* __restrict__ trace_v,
-                                                         int* __restrict__ trace_i) {
+                                                         int* __restrict__ trace_i, int stride) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -1163,7 +1176,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __syncthreads();
   if (trace_H) {
     for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS)
-      trace_H[((size_t)it * n_obj + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
+      trace_H[((size_t)it * stride + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
   }
   __syncthreads();
   // ---- LU with partial pivoting (torch.inverse, optimizer.py:188)
@@ -1232,7 +1245,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     S.iters_done = it + 1;
     if (it + 1 >= P.iters) S.status = ST_DONE;
     if (trace_v) {
-      float* tv = trace_v + ((size_t)it * n_obj + o) * TRACE_V;
+      float* tv = trace_v + ((size_t)it * stride + o) * TRACE_V;
       for (int i = 0; i < NPAR; ++i) { tv[i] = bv[i]; tv[NPAR + i] = dx[i]; }
       tv[2 * NPAR + 0] = scal[0];
       tv[2 * NPAR + 1] = S.sdf_loss;
@@ -1242,8 +1255,8 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     }
   }
   if (trace_i && tid == 0) {
-    trace_i[((size_t)it * n_obj + o) * 2 + 0] = S.n_valid;
-    trace_i[((size_t)it * n_obj + o) * 2 + 1] = S.k;
+    trace_i[((size_t)it * stride + o) * 2 + 0] = S.n_valid;
+    trace_i[((size_t)it * stride + o) * 2 + 1] = S.k;
   }
 }
 
@@ -1287,11 +1300,11 @@ __global__ void k_inv_out(const ObjState* __restrict__ st, float* __restrict__ o
 
 // per-iteration counters for the algorithmic-FLOP bookkeeping
 __global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                        int it, int* __restrict__ counts) {
+                        int it, int* __restrict__ counts, int stride) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= n_obj) return;
   const ObjState& S = st[o];
-  int* c = counts + ((size_t)it * n_obj + o) * 3;
+  int* c = counts + ((size_t)it * stride + o) * 3;
   c[0] = S.n_eval;
   c[1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
   c[2] = S.n_valid;

@@ -38,10 +38,11 @@ struct Fwd16Shared {
 };
 
 // one 32-k step of the 3-product MFMA block for a 64x64 wave tile
-template <bool PRIO, int NQ>
+template <bool PRIO, int NQ, int EX = 0>
 __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&al)[NQ], const half8 (&bh)[4],
                                            const half8 (&bl)[4], floatx4 (&acc)[NQ][4]) {
   if (PRIO) __builtin_amdgcn_s_setprio(1);
+  if constexpr ((EX & 1) == 0) {       // EX bit0: timing experiment, hi.hi product only
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -52,6 +53,7 @@ __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
       acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bl[cb], acc[q][cb], 0, 0, 0);
+  }
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -128,9 +130,12 @@ __device__ __forceinline__ void gemm16_tile_x(const half8* __restrict__ A, int T
   }
 }
 
-template <bool PRIO, int NQ = 4>
+// EX: timing experiments only (invalid results): bit0 one MFMA product per block,
+// bit1 every k step re-reads the first step's A fragments (no L2 streaming).
+template <bool PRIO, int NQ = 4, int EX = 0>
 __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
                                             const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane) {
+  constexpr int TS = (EX & 2) ? 0 : 1;
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -148,27 +153,27 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
   for (int t = 0; t < T; t += 2) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      ah1[q] = A[((q * T + t + 1) * 2 + 0) * 64 + lane];
-      al1[q] = A[((q * T + t + 1) * 2 + 1) * 64 + lane];
+      ah1[q] = A[((q * T + TS * (t + 1)) * 2 + 0) * 64 + lane];
+      al1[q] = A[((q * T + TS * (t + 1)) * 2 + 1) * 64 + lane];
     }
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       bh1[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 1));
       bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
     }
-    mfma3_step<PRIO, NQ>(ah0, al0, bh0, bl0, acc);
+    mfma3_step<PRIO, NQ, EX>(ah0, al0, bh0, bl0, acc);
     const int tn = (t + 2 < T) ? t + 2 : T - 1;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      ah0[q] = A[((q * T + tn) * 2 + 0) * 64 + lane];
-      al0[q] = A[((q * T + tn) * 2 + 1) * 64 + lane];
+      ah0[q] = A[((q * T + TS * tn) * 2 + 0) * 64 + lane];
+      al0[q] = A[((q * T + TS * tn) * 2 + 1) * 64 + lane];
     }
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * tn);
       bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * tn);
     }
-    mfma3_step<PRIO, NQ>(ah1, al1, bh1, bl1, acc);
+    mfma3_step<PRIO, NQ, EX>(ah1, al1, bh1, bl1, acc);
   }
 }
 
@@ -278,6 +283,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   const int nt = *n_tiles;
   constexpr bool XP = (X & 1) != 0;
   constexpr int EXPM = X & 6;
+  constexpr int EX = (X >> 3) & 3;
   const int T1 = D.Kf[1] / 32;
   half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
   if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
                                wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
       } else {
-        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
+        gemm16_tile<PRIO, 4, EX>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
       }
       if constexpr (EXPM == 0) {
         sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
@@ -357,7 +363,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
                                wfrag(D.Wh_raw[1], w, T1), T1);
       else
-        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
+        gemm16_tile<PRIO, 4, EX>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)

@@ -164,8 +164,11 @@ def test_trajectory_shadowing_and_final(gpu_decoder, oracle_dec, name, optim, dt
     assert np.isfinite(t["loss"]).all()
 
 
-def test_batch_equals_single(gpu_decoder):
-    """Objects in a batch are independent: batched results == one-by-one, bitwise."""
+@pytest.mark.parametrize("streams", ["1", "2", "3", "4"])
+def test_batch_equals_single(gpu_decoder, streams, monkeypatch):
+    """Objects in a batch are independent: batched results == one-by-one, bitwise, however
+    the batch is split into object groups on concurrent streams (DSR_STREAMS)."""
+    monkeypatch.setenv("DSR_STREAMS", streams)
     opt = _opt(gpu_decoder, dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
                                                                     num_iterations=3)), "Redwood")
     objs = []
@@ -173,14 +176,17 @@ def test_batch_equals_single(gpu_decoder):
         o = S.make_object(300 + i, n_pts=200 + 97 * i, n_bg=50 + 10 * i, scale=1.0, tz=3.0,
                           upright=False)
         objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
-    batch = opt.reconstruct_objects(objs)
+    batch, tr = opt.reconstruct_objects(objs, trace=True)
     for i, ob in enumerate(objs):
-        single = opt.reconstruct_object(*ob[:4])
+        single, tr1 = opt.reconstruct_objects([ob], trace=True)
+        single = single[0]
         assert batch[i]["is_good"] == single["is_good"]
         if single["is_good"]:
             assert np.array_equal(batch[i]["t_cam_obj"], single["t_cam_obj"])
             assert np.array_equal(batch[i]["code"], single["code"])
             assert batch[i]["loss"] == single["loss"]
+        for key in ("H", "b", "loss", "n_valid", "k"):
+            assert np.array_equal(tr[i][key], tr1[0][key]), (i, key)
 
 
 def test_failure_cases(gpu_decoder):
@@ -377,6 +383,7 @@ def test_early_ray_termination_matches_full_decode(gpu_decoder, monkeypatch):
 
     params = L.optim_params(one)
     pts = {}
+    monkeypatch.setenv("DSR_STREAMS", "1")
     for spec in ("0", "8,12,16,20,24,32"):
         monkeypatch.setenv("DSR_RENDER_PASSES", spec)
         h, keep = bench.make_batch(gpu_decoder, params, 8, 1000)
