@@ -14,6 +14,7 @@
 
 #include "../../include/dsr.h"
 #include "dsr_kernels.hpp"
+#include "dsr_mc.hpp"
 
 #ifndef DSR_DEFAULT_FWD_VARIANT
 #define DSR_DEFAULT_FWD_VARIANT 12  // split-fp16 (3xFP16) + s_setprio (A/B: tools/fwd_variants.py)
@@ -772,6 +773,129 @@ __global__ void k_fold_code(DevDecoder D, const float* __restrict__ z, float* __
   }
   bias0f[n] = D.bias[0][n] + s0;
   bias4f[n] = D.bias[4][n] + s4;
+}
+
+// ------------------------------------------------------------------------------------
+// mesh extraction (MeshExtractor, optimizer.py:216-233; utils.py:119-140)
+// ------------------------------------------------------------------------------------
+struct dsr_mesher {
+  dsr_ctx* ctx = nullptr;
+  const dsr_decoder* dec = nullptr;
+  int d = 0, n = 0, nt = 0;
+  std::vector<void*> allocs;
+  float4* pts = nullptr;       // grid points (x,y,z, bits(index)), tile-padded
+  Tile* tiles = nullptr;
+  int* ntiles = nullptr;
+  ObjDesc* desc = nullptr;
+  float *code = nullptr, *b0 = nullptr, *b4 = nullptr, *vol = nullptr;
+  int *flag = nullptr, *vidx = nullptr, *ntri = nullptr, *toff = nullptr, *bsum = nullptr, *tot = nullptr;
+  float* verts = nullptr;
+  int* faces = nullptr;
+};
+
+int dsr_mesher_destroy(dsr_mesher* m) {
+  if (!m) return 0;
+  hipSetDevice(m->ctx->device);
+  for (void* p : m->allocs) hipFree(p);
+  delete m;
+  return 0;
+}
+
+int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pts, int vol_dim,
+                      dsr_mesher** out) {
+  if (!ctx || !dec || !grid_pts || !out) return fail(ctx, "null argument");
+  *out = nullptr;
+  if (vol_dim < 2 || vol_dim > 512) return fail(ctx, "vol_dim must be in [2, 512]");
+  hipSetDevice(ctx->device);
+  auto* m = new dsr_mesher();
+  m->ctx = ctx;
+  m->dec = dec;
+  m->d = vol_dim;
+  m->n = vol_dim * vol_dim * vol_dim;
+  m->nt = (m->n + TILE - 1) / TILE;
+  const int d = vol_dim, n = m->n, nt = m->nt, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
+  const int nb = (std::max(ne, nc) + MC_SCAN_BLOCK - 1) / MC_SCAN_BLOCK;
+  auto A = [&](void** p, size_t bytes) {
+    if (hipMalloc(p, std::max<size_t>(bytes, 4)) != hipSuccess) return false;
+    m->allocs.push_back(*p);
+    return true;
+  };
+  if (!A((void**)&m->pts, sizeof(float4) * (size_t)nt * TILE) || !A((void**)&m->tiles, sizeof(Tile) * nt) ||
+      !A((void**)&m->ntiles, sizeof(int)) || !A((void**)&m->desc, sizeof(ObjDesc)) ||
+      !A((void**)&m->code, sizeof(float) * CODE) || !A((void**)&m->b0, sizeof(float) * HID) ||
+      !A((void**)&m->b4, sizeof(float) * HID) || !A((void**)&m->vol, sizeof(float) * (size_t)nt * TILE) ||
+      !A((void**)&m->flag, sizeof(int) * (size_t)ne) || !A((void**)&m->vidx, sizeof(int) * (size_t)ne) ||
+      !A((void**)&m->ntri, sizeof(int) * (size_t)nc) || !A((void**)&m->toff, sizeof(int) * (size_t)nc) ||
+      !A((void**)&m->bsum, sizeof(int) * (size_t)nb) || !A((void**)&m->tot, sizeof(int) * 2) ||
+      !A((void**)&m->verts, sizeof(float) * 3 * (size_t)ne) ||
+      !A((void**)&m->faces, sizeof(int) * 3 * (size_t)DSR_MC_MAX_TRI * nc)) {
+    dsr_mesher_destroy(m);
+    return fail(ctx, "hipMalloc failed (mesher)");
+  }
+  std::vector<float4> hp((size_t)nt * TILE, make_float4(0.f, 0.f, 0.f, 0.f));
+  for (int i = 0; i < n; ++i) {
+    float fi;
+    std::memcpy(&fi, &i, sizeof(float));
+    hp[i] = make_float4(grid_pts[(size_t)i * 3], grid_pts[(size_t)i * 3 + 1], grid_pts[(size_t)i * 3 + 2], fi);
+  }
+  std::vector<Tile> ht(nt);
+  for (int t = 0; t < nt; ++t) ht[t] = Tile{0, 0, t * TILE, std::min(TILE, n - t * TILE)};
+  ObjDesc od{};
+  od.n_pts = n;
+  if (hipMemcpy(m->pts, hp.data(), sizeof(float4) * hp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m->tiles, ht.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m->ntiles, &nt, sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m->desc, &od, sizeof(ObjDesc), hipMemcpyHostToDevice) != hipSuccess) {
+    dsr_mesher_destroy(m);
+    return fail(ctx, "hipMemcpy failed (mesher)");
+  }
+  *out = m;
+  return 0;
+}
+
+static void mc_scan(hipStream_t s, const int* in, int n, int* out, int* bsum, int* total) {
+  const int nb = (n + MC_SCAN_BLOCK - 1) / MC_SCAN_BLOCK;
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(MC_SCAN_BLOCK), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(MC_SCAN_BLOCK), 0, s, bsum, nb, total);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(MC_SCAN_BLOCK), 0, s, in, n, (const int*)bsum, out);
+}
+
+int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, int vcap, int* faces,
+                   int fcap, int* n_verts, int* n_faces) {
+  if (!m || !code || !n_verts || !n_faces) return fail(m ? m->ctx : nullptr, "null argument");
+  dsr_ctx* ctx = m->ctx;
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  const int d = m->d, n = m->n, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
+  const DevDecoder& D = m->dec->D;
+  DSR_CHECK(ctx, hipMemcpyAsync(m->code, code, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)m->code, m->b0, m->b4);
+  hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
+                     (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
+                     (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
+                     ErtArgs{nullptr, 1, 0.f});
+  const int B = 256;
+  hipLaunchKernelGGL(k_mc_edges, dim3((n + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->flag);
+  hipLaunchKernelGGL(k_mc_cells, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->ntri);
+  mc_scan(s, m->flag, ne, m->vidx, m->bsum, m->tot);
+  mc_scan(s, m->ntri, nc, m->toff, m->bsum, m->tot + 1);
+  hipLaunchKernelGGL(k_mc_verts, dim3((ne + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level,
+                     2.0 / (double)(d - 1), (const int*)m->flag, (const int*)m->vidx, m->verts);
+  hipLaunchKernelGGL(k_mc_faces, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level,
+                     (const int*)m->vidx, (const int*)m->toff, m->faces);
+  DSR_CHECK(ctx, hipGetLastError());
+  int tot[2];
+  DSR_CHECK(ctx, hipMemcpyAsync(tot, m->tot, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+  DSR_CHECK(ctx, hipStreamSynchronize(s));
+  *n_verts = tot[0];
+  *n_faces = tot[1];
+  if (tot[0] > vcap || tot[1] > fcap || (tot[0] > 0 && !verts) || (tot[1] > 0 && !faces)) {
+    fail(ctx, "mesh larger than the given capacity");
+    return -5;
+  }
+  if (tot[0] > 0) DSR_CHECK(ctx, hipMemcpy(verts, m->verts, sizeof(float) * 3 * tot[0], hipMemcpyDeviceToHost));
+  if (tot[1] > 0) DSR_CHECK(ctx, hipMemcpy(faces, m->faces, sizeof(int) * 3 * tot[1], hipMemcpyDeviceToHost));
+  return 0;
 }
 
 int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts, int n,

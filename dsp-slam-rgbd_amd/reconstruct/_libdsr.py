@@ -94,6 +94,9 @@ SIGNATURES = {
     "dsr_sdf_eval": (C.c_int, [C.c_void_p, C.c_void_p, FP, FP, C.c_int, FP, FP]),
     "dsr_pose_only": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), FP, C.c_float,
                                 FP, C.c_int, FP, FP]),
+    "dsr_mesher_create": (C.c_int, [C.c_void_p, C.c_void_p, FP, C.c_int, C.POINTER(C.c_void_p)]),
+    "dsr_mesher_run": (C.c_int, [C.c_void_p, FP, C.c_float, FP, C.c_int, IP, C.c_int, IP, IP]),
+    "dsr_mesher_destroy": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None

@@ -188,20 +188,51 @@ def sdf_eval(decoder, code, pts, with_jac=False):
 
 
 class MeshExtractor(object):
-    """optimizer.py:216-233."""
+    """optimizer.py:216-233 — grid decode + marching cubes on device (dsr_mesher_*).
+
+    The voxel grid is reconstruct.utils.create_voxel_grid (bit-exact, including the
+    reference's true-division shear) and is uploaded once, like the reference builds it
+    once in __init__.  The reference meshes with skimage.measure.marching_cubes_lewiner
+    (utils.py:119-140); the build's marching cubes (dsr_mc.hpp) is a closed,
+    consistently oriented surface through the same level set — vertex/face ORDER and
+    the triangulation of ambiguous cells are its own (parity unpinned: skimage is absent,
+    DESIGN.md §3.5)."""
 
     def __init__(self, decoder, code_len=64, voxels_dim=64):
         self.decoder = decoder
         self.code_len = code_len
         self.voxels_dim = voxels_dim
         self.voxel_points = create_voxel_grid(vol_dim=self.voxels_dim)
+        ctx = decoder.ctx
+        h = C.c_void_p()
+        ctx.check(ctx.lib.dsr_mesher_create(ctx.handle, decoder.handle, L.fptr(self.voxel_points),
+                                            self.voxels_dim, C.byref(h)), "dsr_mesher_create")
+        self._h = h
+        d = self.voxels_dim
+        self._verts = np.zeros((3 * d ** 3, 3), np.float32)
+        self._faces = np.zeros((5 * (d - 1) ** 3, 3), np.int32)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self.decoder.ctx.lib.dsr_mesher_destroy(h)
+            except Exception:
+                pass
+            self._h = None
 
     def decode_grid(self, code):
         """The (voxels_dim^3,) SDF grid of optimizer.py:226 (decode_sdf on device)."""
         return sdf_eval(self.decoder, np.asarray(code)[:self.code_len], self.voxel_points)
 
-    def extract_mesh_from_code(self, code):
-        from reconstruct.mesh import marching_cubes_lewiner_like
+    def extract_mesh_from_code(self, code, level=0.0):
+        ctx = self.decoder.ctx
+        c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1)[:self.code_len])
+        nv, nf = C.c_int(), C.c_int()
+        ctx.check(ctx.lib.dsr_mesher_run(self._h, L.fptr(c), float(level), L.fptr(self._verts),
+                                         self._verts.shape[0], L.iptr(self._faces), self._faces.shape[0],
+                                         C.byref(nv), C.byref(nf)), "dsr_mesher_run")
+        return ForceKeyErrorDict(vertices=self._verts[:nv.value].copy(), faces=self._faces[:nf.value].copy())
 
         sdf = self.decode_grid(code).reshape(self.voxels_dim, self.voxels_dim, self.voxels_dim)
         vertices, faces = marching_cubes_lewiner_like(sdf)

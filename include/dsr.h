@@ -166,6 +166,21 @@ int dsr_batch_destroy(dsr_batch* b);
 int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts,
                  int n, float* sdf, float* jac);
 
+/* ---- mesh extraction: replaces MeshExtractor (optimizer.py:216-233) with
+ * convert_sdf_voxels_to_mesh (utils.py:119-140).  `grid_pts` is the (vol_dim^3 x 3)
+ * voxel grid of reconstruct.utils.create_voxel_grid (uploaded once, like the reference's
+ * MeshExtractor.__init__); dsr_mesher_run decodes it with `code`, runs marching cubes
+ * at `level` on device and copies out vertices (n_verts x 3, float) and faces
+ * (n_faces x 3, int).  Worst-case capacities: 3*vol_dim^3 vertices and
+ * 5*(vol_dim-1)^3 faces; on a smaller capacity the counts are still returned with
+ * status -5 and nothing is copied. */
+typedef struct dsr_mesher dsr_mesher;
+int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pts, int vol_dim,
+                      dsr_mesher** out);
+int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, int vcap, int* faces,
+                   int fcap, int* n_verts, int* n_faces);
+int dsr_mesher_destroy(dsr_mesher* m);
+
 /* ---- pose-only SE(3) GN: replaces Optimizer.estimate_pose_cam_obj
  * (optimizer.py:46-87).  t_co_se3: 4x4 SE(3) camera<-object, scale: object scale,
  * result written to t_out (4x4). */
