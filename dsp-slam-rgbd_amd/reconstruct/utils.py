@@ -74,3 +74,39 @@ def create_voxel_grid(vol_dim=128):
     values[:, 1] = values[:, 1] * np.float32(voxel_size) + np.float32(voxel_origin[1])
     values[:, 2] = values[:, 2] * np.float32(voxel_size) + np.float32(voxel_origin[0])
     return values
+
+
+
+# PLY layout plyfile.PlyData([vertex(x,y,z f4), face(vertex_indices i4 x3)]).write() produces
+# (utils.py:143-161): binary, native (little-endian) byte order, list counts as uchar.
+_PLY_HEADER = ("ply\nformat binary_little_endian 1.0\nelement vertex {nv}\nproperty float x\n"
+               "property float y\nproperty float z\nelement face {nf}\n"
+               "property list uchar int vertex_indices\nend_header\n")
+
+
+def write_mesh_to_ply(v, f, ply_filename_out):
+    """utils.py:141-161 without plyfile: the same binary PLY."""
+    v = np.ascontiguousarray(v, dtype="<f4").reshape(-1, 3)
+    f = np.ascontiguousarray(f, dtype="<i4").reshape(-1, 3)
+    rec = np.zeros(f.shape[0], dtype=[("n", "u1"), ("idx", "<i4", (3,))])
+    rec["n"] = 3
+    rec["idx"] = f
+    with open(ply_filename_out, "wb") as fh:
+        fh.write(_PLY_HEADER.format(nv=v.shape[0], nf=f.shape[0]).encode("ascii"))
+        fh.write(v.tobytes())
+        fh.write(rec.tobytes())
+
+
+def read_mesh_ply(path):
+    """Inverse of write_mesh_to_ply (triangle meshes in that layout only)."""
+    with open(path, "rb") as fh:
+        data = fh.read()
+    end = data.index(b"end_header\n") + len(b"end_header\n")
+    head = data[:end].decode("ascii").split("\n")
+    nv = int(next(x for x in head if x.startswith("element vertex")).split()[-1])
+    nf = int(next(x for x in head if x.startswith("element face")).split()[-1])
+    v = np.frombuffer(data, dtype="<f4", count=3 * nv, offset=end).reshape(nv, 3)
+    rec = np.frombuffer(data, dtype=[("n", "u1"), ("idx", "<i4", (3,))], count=nf, offset=end + 12 * nv)
+    if nf and not np.all(rec["n"] == 3):
+        raise ValueError("not a triangle mesh")
+    return v.copy(), rec["idx"].copy()

@@ -427,3 +427,23 @@ def test_mesh_extractor_matches_oracle_and_level_set(gpu_decoder):
         shear = np.array([[1.0, 1.0 / d, 1.0 / d ** 2], [0.0, 1.0, 1.0 / d], [0.0, 0.0, 1.0]])
         s = sdf_eval(gpu_decoder, code, (h * q @ shear.T - 1.0).astype(np.float32))
         assert np.median(np.abs(s)) < 0.02 * h and np.abs(s).max() < 0.5 * h
+
+
+def test_extract_map_objects_end_to_end(gpu_decoder, tmp_path):
+    """MapObjects.txt -> objects/<id>.npy + .ply (extract_map_objects.py:46-63) on device."""
+    from reconstruct.map_objects import extract_map_objects, write_map_objects
+    from reconstruct.optimizer import MeshExtractor
+    from reconstruct.utils import read_mesh_ply
+
+    rng = np.random.default_rng(3)
+    objs = [(i, np.eye(4, dtype=np.float32), (0.2 * rng.standard_normal(64)).astype(np.float32))
+            for i in (4, 9)]
+    write_map_objects(str(tmp_path / "MapObjects.txt"), objs)
+    ex = MeshExtractor(gpu_decoder, 64, 32)
+    assert extract_map_objects(str(tmp_path), ex) == [4, 9]
+    for oid, _, code in objs:
+        pose = np.load(tmp_path / "objects" / f"{oid}.npy")
+        assert np.array_equal(pose, np.eye(4))
+        v, f = read_mesh_ply(str(tmp_path / "objects" / f"{oid}.ply"))
+        m = ex.extract_mesh_from_code(np.float32(np.round(code.astype(np.float64), 9)))
+        assert np.array_equal(v, m.vertices) and np.array_equal(f, m.faces) and f.shape[0] > 100
