@@ -445,5 +445,5 @@ def test_extract_map_objects_end_to_end(gpu_decoder, tmp_path):
         pose = np.load(tmp_path / "objects" / f"{oid}.npy")
         assert np.array_equal(pose, np.eye(4))
         v, f = read_mesh_ply(str(tmp_path / "objects" / f"{oid}.ply"))
-        m = ex.extract_mesh_from_code(np.float32(np.round(code.astype(np.float64), 9)))
+        m = ex.extract_mesh_from_code(np.asarray([float(f"{x:.9f}") for x in code], np.float32))
         assert np.array_equal(v, m.vertices) and np.array_equal(f, m.faces) and f.shape[0] > 100
