@@ -135,12 +135,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # DSR_BENCH_BACKEND=gloo (host tensors) rehearses the N>1 code path with several ranks on
+    # one device, which RCCL refuses; the driver's runs use RCCL ("nccl") over xGMI
+    backend = os.environ.get("DSR_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+            local = local % max(1, torch.cuda.device_count())
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
 
     from deep_sdf.workspace import decoder_from_state
     from reconstruct import _libdsr as L
@@ -166,7 +174,7 @@ def main():
         if dist is not None:
             import torch
 
-            t = torch.from_numpy(rec).cuda()
+            t = torch.from_numpy(rec).to(coll_dev)
             gath = torch.empty((world * n_obj, 96), dtype=torch.float32, device=t.device)
             dist.all_gather_into_tensor(gath, t)       # RCCL over xGMI
             torch.cuda.synchronize()
@@ -204,7 +212,7 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_obj = n_obj * world * args.steps
