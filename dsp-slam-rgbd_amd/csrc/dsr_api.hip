@@ -61,9 +61,9 @@ static FwdKernel fwd_kernel(int v) {
 using JacKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const ObjState*, const float*,
                            const float4*, const float*, const float*, const float*, GNParams, float*,
                            const float4*, float*, float*);
+static int jac_variant();
 static JacKernel jac_kernel() {
-  const char* e = getenv("DSR_JAC_VARIANT");
-  const int v = e ? atoi(e) : 12;
+  const int v = jac_variant();
   switch (v) {
     case 8: return k_mlp_jac16<false, false>;
     case 12: return k_mlp_jac16<true, false>;
@@ -130,6 +130,10 @@ struct dsr_batch {
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
+  int runs = 0;
+  bool timed = false;               // last run recorded per-kernel events (eager run)
+  hipGraphExec_t graph = nullptr;   // the whole run, captured on the 2nd dsr_batch_run
+  long graph_key = -1;              // kernel variants the graph was captured with
 };
 
 #define DSR_CHECK(ctx, call)                                                        \
@@ -447,6 +451,7 @@ int dsr_batch_destroy(dsr_batch* b) {
   if (!b) return 0;
   hipSetDevice(b->ctx->device);
   for (auto& e : b->ev) hipEventDestroy(e);
+  if (b->graph) hipGraphExecDestroy(b->graph);
   for (auto& e : b->join_ev) hipEventDestroy(e);
   if (b->fork_ev) hipEventDestroy(b->fork_ev);
   for (void* p : b->allocs) hipFree(p);
@@ -598,10 +603,74 @@ int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_param
   return batch_create_impl(ctx, dec, p, n_obj, in, false, out);
 }
 
+static int batch_enqueue(dsr_batch* b, bool timing = true);
+
+static int jac_variant() {
+  const char* e = getenv("DSR_JAC_VARIANT");
+  return e ? atoi(e) : 12;
+}
+
+// dsr_batch_run: with DSR_GRAPH=1 the first run of a batch is enqueued eagerly and from
+// the second on (a re-run batch: streaming keyframes, config 5) the whole multi-stream
+// launch sequence — ~6 + 3 x passes launches per iteration and group — is captured once
+// into a hipGraph and replayed with one launch; dsr_batch_graph captures up front.  A
+// replayed run records only its total time (kernel events stay out of the graph: HIP
+// cannot time events recorded inside one), so dsr_batch_stats reports no kernel times.
+static bool graph_enabled() {        // DSR_GRAPH=1: replay re-run batches as hipGraphs
+  const char* ge = getenv("DSR_GRAPH");
+  return ge && atoi(ge) != 0;
+}
+static long graph_key() { return (long)fwd_variant() * 100000 + jac_variant(); }
+
+static int batch_capture(dsr_batch* b) {
+  dsr_ctx* ctx = b->ctx;
+  if (b->graph) {
+    hipGraphExecDestroy(b->graph);
+    b->graph = nullptr;
+  }
+  hipGraph_t g = nullptr;
+  DSR_CHECK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  const int rc = batch_enqueue(b, false);      // kernel timing events stay out of the graph
+  const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
+  if (rc) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  DSR_CHECK(ctx, ec);
+  const hipError_t ei = hipGraphInstantiate(&b->graph, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  DSR_CHECK(ctx, ei);
+  b->graph_key = graph_key();
+  return 0;
+}
+
+int dsr_batch_graph(dsr_batch* b) {
+  if (!b) return -2;
+  hipSetDevice(b->ctx->device);
+  if (!graph_enabled()) return 0;
+  b->runs = std::max(b->runs, 1);
+  return batch_capture(b);
+}
+
 int dsr_batch_run(dsr_batch* b) {
   if (!b) return -2;
   dsr_ctx* ctx = b->ctx;
   hipSetDevice(ctx->device);
+  if (!graph_enabled() || b->runs++ == 0) return batch_enqueue(b);
+  if (!b->graph || b->graph_key != graph_key()) {
+    const int rc = batch_capture(b);
+    if (rc) return rc;
+  }
+  DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
+  DSR_CHECK(ctx, hipGraphLaunch(b->graph, ctx->stream));
+  DSR_CHECK(ctx, hipEventRecord(b->ev[1], ctx->stream));
+  b->ran = true;
+  b->timed = false;
+  return 0;
+}
+
+static int batch_enqueue(dsr_batch* b, bool timing) {
+  dsr_ctx* ctx = b->ctx;
   hipStream_t s0 = ctx->stream;
   const int n = b->n_obj;
   const DevDecoder& D = b->dec->D;
@@ -614,7 +683,7 @@ int dsr_batch_run(dsr_batch* b) {
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
-  DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
+  if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
   hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s0, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
   DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
   for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
@@ -635,19 +704,19 @@ int dsr_batch_run(dsr_batch* b) {
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
-        DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
         hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
                            b0, b4, b->dense, gr.sync, ErtArgs{b->dead, b->M, -P.cut_off});
-        DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
       }
       hipLaunchKernelGGL(k_render, dim3(ng), dim3(RENDER_THREADS), 0, s, ng, desc, st, b->rays, b->dobs, P,
                          b->dense, b->kpts, b->kres);
       hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
-      DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
                          b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
                          (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
-      DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
       hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
                          b->counts + (size_t)o0 * 3, n);
       hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, b->slots,
@@ -662,8 +731,9 @@ int dsr_batch_run(dsr_batch* b) {
   }
   hipLaunchKernelGGL(k_finalize, dim3(cb), dim3(64), 0, s0, n, b->st, b->zbuf, b->out);
   DSR_CHECK(ctx, hipGetLastError());
-  DSR_CHECK(ctx, hipEventRecord(b->ev[1], s0));
+  if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[1], s0));
   b->ran = true;
+  b->timed = timing;
   return 0;
 }
 
@@ -693,7 +763,7 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
-  for (int it = 0; it < b->iters; ++it)
+  for (int it = 0; it < (b->timed ? b->iters : 0); ++it)
     for (int g = 0; g < G; ++g) {
       const hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       for (int pz = 0; pz < np; ++pz) {
@@ -705,8 +775,8 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
     }
   DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
   st->total_ms = ms;
-  st->fwd_launches = b->iters * np * G;
-  st->jac_launches = b->iters * G;
+  st->fwd_launches = b->timed ? b->iters * np * G : 0;
+  st->jac_launches = b->timed ? b->iters * G : 0;
   std::vector<int> c((size_t)3 * std::max(1, b->iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < b->iters; ++it)

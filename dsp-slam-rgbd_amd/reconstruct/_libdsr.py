@@ -87,6 +87,7 @@ SIGNATURES = {
     "dsr_batch_create": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int,
                                    C.POINTER(ObjectIn), C.POINTER(C.c_void_p)]),
     "dsr_batch_run": (C.c_int, [C.c_void_p]),
+    "dsr_batch_graph": (C.c_int, [C.c_void_p]),
     "dsr_batch_sync": (C.c_int, [C.c_void_p]),
     "dsr_batch_download": (C.c_int, [C.c_void_p, C.POINTER(ObjectOut)]),
     "dsr_batch_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),

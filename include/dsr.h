@@ -152,7 +152,9 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
  * the context stream). */
 int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
                      int n_obj, const dsr_object_in* in, dsr_batch** out);
-int dsr_batch_run(dsr_batch* b);                  /* async on the context stream */
+int dsr_batch_run(dsr_batch* b);                  /* async on the context stream; with
+                                                      DSR_GRAPH=1 re-runs replay a hipGraph */
+int dsr_batch_graph(dsr_batch* b);                /* capture that graph now (DSR_GRAPH=1) */
 int dsr_batch_sync(dsr_batch* b);
 int dsr_batch_download(dsr_batch* b, dsr_object_out* out);
 int dsr_batch_stats(dsr_batch* b, dsr_stats* st);

@@ -447,3 +447,35 @@ def test_extract_map_objects_end_to_end(gpu_decoder, tmp_path):
         v, f = read_mesh_ply(str(tmp_path / "objects" / f"{oid}.ply"))
         m = ex.extract_mesh_from_code(np.asarray([float(f"{x:.9f}") for x in code], np.float32))
         assert np.array_equal(v, m.vertices) and np.array_equal(f, m.faces) and f.shape[0] > 100
+
+
+def test_graph_replay_bitwise(gpu_decoder, monkeypatch):
+    """DSR_GRAPH=1: a re-run batch is captured into a hipGraph (2nd run) and replayed (3rd):
+    results and per-iteration counters identical to the eager first run."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    params = L.optim_params(dict(S.REDWOOD_OPTIM))
+    for graph in ("1", "0"):
+        monkeypatch.setenv("DSR_GRAPH", graph)
+        h, keep = bench.make_batch(gpu_decoder, params, 6, 4000)
+        try:
+            sig = []
+            for _ in range(3):
+                outs = (L.ObjectOut * 6)()
+                ctx.check(lib.dsr_batch_run(h), "run")
+                ctx.check(lib.dsr_batch_download(h, outs), "download")
+                st = L.Stats()
+                ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+                assert st.total_ms > 0
+                replay = graph == "1" and len(sig) > 0
+                assert (st.fwd_launches == 0) if replay else (st.fwd_ms > 0 and st.jac_ms > 0)
+                sig.append((np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good] for o in outs],
+                                     np.float32), st.fwd_points, st.jac_points, st.inball_points))
+            for s in sig[1:]:
+                assert np.array_equal(s[0], sig[0][0]) and s[1:] == sig[0][1:]
+        finally:
+            lib.dsr_batch_destroy(h)
