@@ -413,10 +413,13 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // ------------------------------------------------------------------------------------
 // Render-pass schedule of the early ray termination (k_sample_pass): in-ball rank
 // boundaries, DSR_RENDER_PASSES="8,12,16,20,24,32" style (ascending, each < M); one pass
-// [0, M) when empty ("0" disables termination).
-static std::vector<int> render_passes(int M) {
+// [0, M) when empty ("0" disables termination).  Default: fine windows for large batches
+// (fewer wasted samples), coarse ones for small batches whose passes are too short to
+// fill the chip (measured: 64 KITTI objects 186 vs 176 obj/s, 8 Redwood objects 10.6 vs
+// 11.2 ms per batch).
+static std::vector<int> render_passes(int M, long samples) {
   const char* e = getenv("DSR_RENDER_PASSES");
-  std::string spec = e ? e : "8,12,16,20,24,32";
+  std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : "8,16,24");
   std::vector<int> r{0};
   size_t p = 0;
   while (p < spec.size()) {
@@ -580,7 +583,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     hipMemset(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj);
     hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
   }
-  b->passes = render_passes(M);
+  b->passes = render_passes(M, (long)cand_off);
   b->ev.resize((size_t)std::max(1, b->iters) * b->groups.size() * ev_per_iter(b) + 2);
   b->join_ev.resize(b->groups.size());
   for (auto& e : b->ev)
