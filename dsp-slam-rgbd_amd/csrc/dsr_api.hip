@@ -127,6 +127,9 @@ struct dsr_batch {
   float *tr_H = nullptr, *tr_v = nullptr;
   int* tr_i = nullptr;
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
+  unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
+  bool lite = true;             // lite classification pass + exact re-decode of the band
+  float margin = 0.02f;
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
@@ -432,7 +435,7 @@ static std::vector<int> render_passes(int M, long samples) {
   r.push_back(M);
   return r;
 }
-static size_t ev_per_iter(const dsr_batch* b) { return 2 * (b->passes.size() - 1) + 2; }
+static size_t ev_per_iter(const dsr_batch* b) { return 2 * (b->passes.size() - 1 + (b->lite ? 1 : 0)) + 2; }
 
 static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
   if (bytes == 0) bytes = 256;
@@ -543,6 +546,19 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->kpts, sizeof(float4) * (size_t)cand_off);
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
+  {
+    const char* e = getenv("DSR_LITE");
+    b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1);
+    const char* mg = getenv("DSR_LITE_MARGIN");
+    if (mg) b->margin = (float)atof(mg);
+  }
+  if (b->lite) {
+    ALLOC(b->refine, (size_t)std::max(1, cand_off));
+    if (hipMemset(b->refine, 0, (size_t)std::max(1, cand_off)) != hipSuccess) {
+      dsr_batch_destroy(b);
+      return fail(ctx, "hipMemset failed");
+    }
+  }
   ALLOC(b->kres, sizeof(float) * (size_t)cand_off);
   ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
   ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
@@ -556,7 +572,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ALLOC(gr.sync, 8 * 32 * sizeof(unsigned));
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
-  ALLOC(b->counts, sizeof(int) * 3 * (size_t)std::max(1, b->iters) * n_obj);
+  ALLOC(b->counts, sizeof(int) * 4 * (size_t)std::max(1, b->iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
   if (trace) {
     const size_t it = std::max(1, b->iters);
@@ -702,26 +718,42 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       float* b4 = b->bias4f + (size_t)o0 * HID;
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
+      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->margin, b->refine};
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
-        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
+                           b->lite ? LTILE : TILE);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
-        hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                           b0, b4, b->dense, gr.sync, ErtArgs{b->dead, b->M, -P.cut_off});
+        if (b->lite)
+          hipLaunchKernelGGL(k_mlp_fwd_lite<true>, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+                             b->cand, b0, b4, b->dense, ert);
+        else
+          hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                             b0, b4, b->dense, gr.sync, ert);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
       }
+      if (b->lite) {                             // exact split-fp16 decode of the band samples
+        hipLaunchKernelGGL(k_refine_compact, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
+                           b->cand, b->refine);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
+        hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                           b0, b4, b->dense, gr.sync, ErtArgs{nullptr, b->M, -P.cut_off, 0.f, nullptr});
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
+      }
+      const int je = 2 * (np + (b->lite ? 1 : 0));
       hipLaunchKernelGGL(k_render, dim3(ng), dim3(RENDER_THREADS), 0, s, ng, desc, st, b->rays, b->dobs, P,
                          b->dense, b->kpts, b->kres);
       hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
-      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
                          b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
                          (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
-      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
       hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
-                         b->counts + (size_t)o0 * 3, n);
+                         b->counts + (size_t)o0 * 4, n);
       hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, b->slots,
                          b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
                          b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
@@ -773,21 +805,29 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
         DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * pz], ev[2 * pz + 1]));
         st->fwd_ms += ms;
       }
-      DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * np], ev[2 * np + 1]));
+      const int je = 2 * (np + (b->lite ? 1 : 0));
+      if (b->lite) {
+        DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[2 * np], ev[2 * np + 1]));
+        st->refine_ms += ms;
+      }
+      DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, ev[je], ev[je + 1]));
       st->jac_ms += ms;
     }
   DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
   st->total_ms = ms;
   st->fwd_launches = b->timed ? b->iters * np * G : 0;
   st->jac_launches = b->timed ? b->iters * G : 0;
-  std::vector<int> c((size_t)3 * std::max(1, b->iters) * b->n_obj);
+  st->refine_launches = (b->timed && b->lite) ? b->iters * G : 0;
+  st->lite = b->lite ? 1 : 0;
+  std::vector<int> c((size_t)4 * std::max(1, b->iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < b->iters; ++it)
     for (int o = 0; o < b->n_obj; ++o) {
-      const int* e = c.data() + ((size_t)it * b->n_obj + o) * 3;
+      const int* e = c.data() + ((size_t)it * b->n_obj + o) * 4;
       st->fwd_points += e[0];
       st->jac_points += e[1];
       st->inball_points += e[2];
+      st->refine_points += e[3];
     }
   return 0;
 }
@@ -946,7 +986,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
-                     ErtArgs{nullptr, 1, 0.f});
+                     ErtArgs{nullptr, 1, 0.f, 0.f, nullptr});
   const int B = 256;
   hipLaunchKernelGGL(k_mc_edges, dim3((n + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->flag);
   hipLaunchKernelGGL(k_mc_cells, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->ntri);
@@ -1022,7 +1062,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   } else {
     hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
-                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f});
+                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, 0.f, nullptr});
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     cleanup();

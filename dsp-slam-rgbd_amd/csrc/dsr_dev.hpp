@@ -79,7 +79,7 @@ struct ObjState {
   int n_sdf_tiles, n_ren_tiles, slot_ren;   // this iteration's jac tiles
   int n_emit;            // ray samples emitted by the current render pass (fwd tiles)
   int n_eval;            // ray samples decoded this iteration (sum over passes)
-  int pad;
+  int n_refine;          // of which re-decoded exactly after the lite pass
 };
 
 struct Tile {
@@ -92,6 +92,8 @@ struct ErtArgs {
   int* dead;             // [sum n_rays] (nullptr: no flagging, e.g. dsr_sdf_eval)
   int M;                 // samples per ray (grid index = ray * M + j)
   float nth;             // -cut_off
+  float margin;          // lite pass: error margin around +-cut_off (dsr_mlp_lite.hpp)
+  unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
 };
 
 struct GNParams {

@@ -22,6 +22,7 @@
 #include "dsr_dev.hpp"
 #include "dsr_mlp.hpp"
 #include "dsr_mlp16.hpp"
+#include "dsr_mlp_lite.hpp"
 #include "../../include/dsr.h"
 
 namespace dsr {
@@ -227,7 +228,7 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
     S.bg_depth = 1.1f * dmax;                                  // :128
     S.n_valid = 0;
     S.k = 0;
-    S.n_emit = S.n_eval = 0;
+    S.n_emit = S.n_eval = S.n_refine = 0;
   }
   __syncthreads();
   const ObjDesc d = desc[o];
@@ -351,22 +352,73 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
 }
 
 // ------------------------------------------------------------------------------------
+// k_refine_compact: the samples the lite pass left in the +-(th + margin) band
+// (dsr_mlp_lite.hpp), (ray, depth)-ordered into cand for the exact split-fp16 pass;
+// clears the flags it consumes.  One thread per ray, one workgroup per object.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, const ObjDesc* __restrict__ desc,
+                                                                   ObjState* st, const float* __restrict__ rays_all,
+                                                                   int M, float4* __restrict__ cand,
+                                                                   unsigned char* __restrict__ refine) {
+  const int o = blockIdx.x;
+  ObjState& S = st[o];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[o];
+  const float* rays = rays_all + (size_t)d.ray_off * 3;
+  __shared__ int wsum[SAMPLE_THREADS / 64];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
+    const int ray = r0 + tid;
+    unsigned char* f = refine + d.cand_off + (size_t)ray * M;
+    uint64_t bits = 0;
+    if (ray < d.n_rays)
+      for (int j = 0; j < M; ++j)
+        if (f[j]) { bits |= 1ull << j; f[j] = 0; }
+    const int cnt = __popcll(bits);
+    const int inc = wave_incl_scan(cnt, lane);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int off = base_s + inc - cnt;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
+    for (uint64_t m = bits; m; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      const float3 x = ray_sample(rays, S, ray, j);
+      cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int k = 0; k < SAMPLE_THREADS / 64; ++k) t += wsum[k];
+      base_s += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    S.n_emit = base_s;
+    S.n_refine = base_s;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // tile tables (single workgroup)
 // ------------------------------------------------------------------------------------
 __global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                            Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize) {
   __shared__ int base_s;
   if (threadIdx.x == 0) base_s = 0;
   __syncthreads();
   for (int o = 0; o < n_obj; ++o) {
     const ObjState& S = st[o];
     const int n = (S.status == ST_RUNNING) ? S.n_emit : 0;
-    const int nt = (n + TILE - 1) / TILE;
+    const int nt = (n + tsize - 1) / tsize;
     const int b = base_s;
     for (int i = threadIdx.x; i < nt; i += blockDim.x) {
       Tile t;
-      t.obj = o; t.term = 0; t.start = i * TILE;
-      t.count = min(TILE, n - i * TILE);
+      t.obj = o; t.term = 0; t.start = i * tsize;
+      t.count = min(tsize, n - i * tsize);
       tiles[b + i] = t;
     }
     __syncthreads();
@@ -1304,10 +1356,11 @@ __global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjSt
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= n_obj) return;
   const ObjState& S = st[o];
-  int* c = counts + ((size_t)it * stride + o) * 3;
+  int* c = counts + ((size_t)it * stride + o) * 4;
   c[0] = S.n_eval;
   c[1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
   c[2] = S.n_valid;
+  c[3] = S.n_refine;
 }
 
 __global__ void k_finalize(int n_obj, const ObjState* __restrict__ st, const float* __restrict__ zbuf,

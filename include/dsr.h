@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 2
+#define DSR_ABI_VERSION 3
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -123,6 +123,11 @@ typedef struct {
   int64_t jac_points;             /* sum of (N + K) */
   int fwd_launches, jac_launches; /* fwd: one per render pass per iteration */
   int64_t inball_points;          /* sum over iterations/objects of N_valid (in-ball samples) */
+  int lite;                       /* 1: fwd_* is the one-product lite pass (DSR_LITE) and
+                                     refine_* the exact split-fp16 re-decode of its band */
+  int refine_launches;
+  double refine_ms;
+  int64_t refine_points;
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */

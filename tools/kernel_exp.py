@@ -37,8 +37,8 @@ for r in range(a.rounds):
         res[(f, j)].append((st.fwd_ms, st.jac_ms,
                             2 * bench.FWD_MAC * st.fwd_points / (st.fwd_ms * 1e-3) / 1e12,
                             2 * (bench.FWD_MAC + bench.BWD_MAC) * st.jac_points / (st.jac_ms * 1e-3) / 1e12,
-                            st.fwd_points, st.jac_points))
+                            st.fwd_points, st.jac_points, st.refine_ms, st.refine_points))
 for k in combos:
     x = np.median(np.array(res[k]), axis=0)
-    print(f"fwd V{k[0]:3d} {x[0]:7.2f} ms {x[2]:6.1f} TF | jac V{k[1]:3d} {x[1]:6.2f} ms {x[3]:6.1f} TF"
-          f" | pts {int(x[4])} / {int(x[5])}")
+    print(f"fwd V{k[0]:3d} {x[0]:7.2f} ms {x[2]:6.1f} TF | refine {x[6]:6.2f} ms {int(x[7])} pts | "
+          f"jac V{k[1]:3d} {x[1]:6.2f} ms {x[3]:6.1f} TF | pts {int(x[4])} / {int(x[5])}")
