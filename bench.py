@@ -104,8 +104,8 @@ def cpu_baseline(seconds_budget=30.0):
                       f"{P.num_iterations} GN iterations timed ({dt:.1f} s), extrapolated to 10"}
 
 
-def pmc_traffic():
-    """HBM bytes per k_mlp_fwd16 launch from the newest committed rocprofv3 PMC summary
+def pmc_traffic(kernel="k_mlp_fwd16"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_summary.json, written by tools/prof_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes over this same default workload), or None."""
     import glob
@@ -117,7 +117,7 @@ def pmc_traffic():
         except Exception:
             continue
         for name, e in d.get("pmc", {}).items():
-            if "k_mlp_fwd16" in name and "hbm_bytes_per_launch" in e:
+            if kernel in name and "hbm_bytes_per_launch" in e:
                 best = (e["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
     return best
 
@@ -190,6 +190,7 @@ def main():
     t0 = time.perf_counter()
     fwd_ms = jac_ms = 0.0
     fwd_pts = jac_pts = inball_pts = fwd_launches = 0
+    refine_ms, refine_pts, lite_err, lite_margin, lite = 0.0, 0, 0.0, 1e30, False
     n_good = 0
     for _ in range(args.steps):
         step()
@@ -201,6 +202,11 @@ def main():
         jac_pts += st.jac_points
         inball_pts += st.inball_points
         fwd_launches += st.fwd_launches
+        refine_ms += st.refine_ms
+        refine_pts += st.refine_points
+        lite_err = max(lite_err, st.lite_max_err)
+        lite_margin = min(lite_margin, st.lite_min_margin)
+        lite = bool(st.lite)
         n_good += sum(int(outs[i].is_good) for i in range(n_obj))
     ctx.check(lib.dsr_batch_sync(batch), "sync")
     if dist is not None:
@@ -223,12 +229,20 @@ def main():
     job_tf = (fwd_flop + jac_flop) / elapsed / 1e12
     variant = int(os.environ.get("DSR_FWD_VARIANT", "12"))
     if variant & 8:
-        peak_tf = FP16_MFMA_PEAK_TF / SPLIT_PRODUCTS
-        peak_note = ("fp32-equivalent peak of the 3xFP16 split: 2.5 PF dense fp16 MFMA / 3 products; "
-                     "achieved counts algorithmic fp32 FLOPs (executed fp16 MFMA FLOPs = 3x)")
+        split_peak = FP16_MFMA_PEAK_TF / SPLIT_PRODUCTS
+        split_note = ("fp32-equivalent peak of the 3xFP16 split: 2.5 PF dense fp16 MFMA / 3 products; "
+                      "achieved counts algorithmic fp32 FLOPs (executed fp16 MFMA FLOPs = 3x)")
     else:
-        peak_tf = FP32_MFMA_PEAK_TF
-        peak_note = "fp32 MFMA dense peak"
+        split_peak = FP32_MFMA_PEAK_TF
+        split_note = "fp32 MFMA dense peak"
+    if lite:
+        kernel, kname = "k_mlp_fwd_lite", "k_mlp_fwd_lite (one-product fp16 classification pass over ray samples)"
+        peak_tf, peak_note = FP16_MFMA_PEAK_TF, "dense fp16 MFMA peak (one product per MAC, fp32 accumulate)"
+    else:
+        kernel, kname = "k_mlp_fwd16", "k_mlp_fwd16 (decode_sdf on ray samples, 3xFP16)"
+        peak_tf, peak_note = split_peak, split_note
+    refine_flop = 2.0 * FWD_MAC * refine_pts
+    refine_tf = refine_flop / (refine_ms * 1e-3) / 1e12 if refine_ms > 0 else 0.0
     if rank == 0:
         out = {
             "metric": "object-reconstructions/sec (2048 pts, 10 GN iters)",
@@ -242,7 +256,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "mfma_precision": ("3xFP16 split (hi/lo fp16 pieces, power-of-2 scaled, fp32 accumulate; "
+            "mfma_precision": ("ray samples classified by a one-product fp16 pass; every value that "
+                               "reaches an output (band samples, Jacobian points) decoded in 3xFP16 split "
+                               "(hi/lo fp16, fp32 accumulate; fp32-class, parity suite green)") if lite else
+                              ("3xFP16 split (hi/lo fp16 pieces, power-of-2 scaled, fp32 accumulate; "
                                "fp32-class accuracy, parity suite green)") if variant & 8 else "fp32 MFMA",
             "data": "synthetic (seeded DeepSDF 8x512 decoder + KITTI-like objects, SURVEY.md §8d)",
             "config": {"workload": f"{n_obj} objects/GPU x 2048 pts x (2048+200) rays x 50 depth "
@@ -250,7 +267,7 @@ def main():
                                    "batched as north-star 64 objects/GPU)",
                        "objects_per_gpu": n_obj, "pts": 2048, "rays": 2248, "iters": 10,
                        "parallelism": f"object-sharded x{world}"},
-            "roofline": {"bound": "mfma", "kernel": "k_mlp_fwd16 (decode_sdf on ray samples, 3xFP16)",
+            "roofline": {"bound": "mfma", "kernel": kname,
                          "achieved": round(fwd_tf, 3), "peak": round(peak_tf, 1),
                          "unit": "TFLOP/s", "frac": round(fwd_tf / peak_tf, 4),
                          "peak_note": peak_note,
@@ -260,6 +277,11 @@ def main():
                          "avg_launch_ms": fwd_ms / max(1, fwd_launches)},
             "early_ray_termination": {"samples_decoded": fwd_pts, "samples_in_ball": inball_pts,
                                       "decoded_fraction": round(fwd_pts / max(1, inball_pts), 4)},
+            "lite_pass": None if not lite else {
+                "refine_points": refine_pts, "refine_fraction": round(refine_pts / max(1, fwd_pts), 4),
+                "refine_kernel": "k_mlp_fwd16 (3xFP16)", "refine_ms_per_step": refine_ms / args.steps,
+                "refine_tflops": round(refine_tf, 3), "refine_peak": round(split_peak, 1),
+                "max_observed_lite_error": lite_err, "min_margin": lite_margin},
             "job_tflops": round(job_tf, 3),
             "jac_kernel_tflops": round(jac_flop / (jac_ms * 1e-3) / 1e12, 3) if jac_ms > 0 else 0.0,
             "good_fraction": n_good / float(n_obj * args.steps),
@@ -268,7 +290,7 @@ def main():
             "batch_create_ms": LAST_CREATE_S * 1e3,
             "cpu_baseline": None,
         }
-        tr = pmc_traffic()
+        tr = pmc_traffic(kernel)
         if tr is not None:
             out["roofline"]["traffic"] = tr[0]
             out["roofline"]["traffic_source"] = tr[1]

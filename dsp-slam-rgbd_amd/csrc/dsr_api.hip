@@ -129,7 +129,6 @@ struct dsr_batch {
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
   unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
   bool lite = true;             // lite classification pass + exact re-decode of the band
-  float margin = 0.02f;
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
@@ -450,6 +449,10 @@ static GNParams make_params(const dsr_optim_params* p) {
   P.b1 = p->b1; P.b2 = p->b2; P.lr = p->lr; P.s_damp = p->s_damp;
   P.cut_off = p->cut_off; P.iters = p->num_iterations; P.M = p->num_depth_samples;
   P.raw_residual = 0;
+  auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
+  P.lite_margin0 = envf("DSR_LITE_MARGIN", 0.02f);    // dsr_mlp_lite.hpp
+  P.lite_floor = envf("DSR_LITE_FLOOR", 0.005f);
+  P.lite_safety = envf("DSR_LITE_SAFETY", 8.0f);
   return P;
 }
 
@@ -549,8 +552,6 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   {
     const char* e = getenv("DSR_LITE");
     b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1);
-    const char* mg = getenv("DSR_LITE_MARGIN");
-    if (mg) b->margin = (float)atof(mg);
   }
   if (b->lite) {
     ALLOC(b->refine, (size_t)std::max(1, cand_off));
@@ -718,7 +719,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       float* b4 = b->bias4f + (size_t)o0 * HID;
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
-      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->margin, b->refine};
+      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine};
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
@@ -740,7 +741,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                           b0, b4, b->dense, gr.sync, ErtArgs{nullptr, b->M, -P.cut_off, 0.f, nullptr});
+                           b0, b4, b->dense, gr.sync, ErtArgs{nullptr, b->M, -P.cut_off, st, nullptr});
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
       }
       const int je = 2 * (np + (b->lite ? 1 : 0));
@@ -819,6 +820,15 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->jac_launches = b->timed ? b->iters * G : 0;
   st->refine_launches = (b->timed && b->lite) ? b->iters * G : 0;
   st->lite = b->lite ? 1 : 0;
+  if (b->lite) {
+    std::vector<ObjState> hs(b->n_obj);
+    DSR_CHECK(b->ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
+    st->lite_min_margin = 1e30;
+    for (const ObjState& o : hs) {
+      st->lite_max_err = std::max(st->lite_max_err, (double)o.lite_err);
+      if (o.iters_done > 0) st->lite_min_margin = std::min(st->lite_min_margin, (double)o.lite_margin);
+    }
+  }
   std::vector<int> c((size_t)4 * std::max(1, b->iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < b->iters; ++it)
@@ -986,7 +996,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
-                     ErtArgs{nullptr, 1, 0.f, 0.f, nullptr});
+                     ErtArgs{nullptr, 1, 0.f, nullptr, nullptr});
   const int B = 256;
   hipLaunchKernelGGL(k_mc_edges, dim3((n + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->flag);
   hipLaunchKernelGGL(k_mc_cells, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->ntri);
@@ -1062,7 +1072,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   } else {
     hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
-                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, 0.f, nullptr});
+                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr});
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     cleanup();

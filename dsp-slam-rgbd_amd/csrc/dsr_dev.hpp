@@ -80,6 +80,8 @@ struct ObjState {
   int n_emit;            // ray samples emitted by the current render pass (fwd tiles)
   int n_eval;            // ray samples decoded this iteration (sum over passes)
   int n_refine;          // of which re-decoded exactly after the lite pass
+  float lite_margin;     // this iteration's classification margin (dsr_mlp_lite.hpp)
+  float lite_err;        // max |lite - exact| seen on this object's re-decoded samples
 };
 
 struct Tile {
@@ -88,11 +90,12 @@ struct Tile {
 
 // Early ray termination (k_sample_pass): the fwd kernels flag a ray dead once one of its
 // samples decodes to sdf <= -cut_off (occupancy exactly 1, transmittance exactly 0 after it).
+struct ObjState;
 struct ErtArgs {
   int* dead;             // [sum n_rays] (nullptr: no flagging, e.g. dsr_sdf_eval)
   int M;                 // samples per ray (grid index = ray * M + j)
   float nth;             // -cut_off
-  float margin;          // lite pass: error margin around +-cut_off (dsr_mlp_lite.hpp)
+  ObjState* st;          // lite pass: per-object margin; exact re-decode: per-object error
   unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
 };
 
@@ -100,6 +103,9 @@ struct GNParams {
   float k1, k2, k3, k4, b1, b2, lr, s_damp, cut_off;
   int iters, M;
   int raw_residual;      // 1: J^T r with the un-robustified residual (pose-only GN, optimizer.py:71)
+  float lite_margin0;    // lite pass: first-iteration margin
+  float lite_floor;      // ... smallest margin
+  float lite_safety;     // ... margin = max(floor, safety x max observed lite error)
 };
 
 __device__ __forceinline__ float fetch4(const float4& v, int j) {

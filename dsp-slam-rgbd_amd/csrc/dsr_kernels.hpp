@@ -187,6 +187,7 @@ __global__ void k_init_state(int n_obj, const float* __restrict__ t_in, const in
     S.iters_done = 0;
     S.n_valid = S.k = 0;
     S.sdf_loss = S.render_loss = 0.f;
+    S.lite_margin = S.lite_err = 0.f;
   }
 }
 
@@ -229,6 +230,12 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
     S.n_valid = 0;
     S.k = 0;
     S.n_emit = S.n_eval = S.n_refine = 0;
+    if (S.iters_done == 0) {
+      S.lite_margin = P.lite_margin0;
+    } else {
+      const float m = fmaxf(P.lite_floor, P.lite_safety * S.lite_err);
+      S.lite_margin = (m <= 0.1f) ? m : 1e30f;          // beyond: every sample exact
+    }
   }
   __syncthreads();
   const ObjDesc d = desc[o];

@@ -385,6 +385,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
       if (px != px || py != py || pz != pz || zprobe != zprobe) y = __builtin_nanf("");
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
+      if (E.st) {                        // re-decode of a lite band sample: track the lite error
+        const float e = fabsf(y - dense[d.cand_off + idx]);
+        if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+      }
       dense[d.cand_off + idx] = y;
       if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
     }

@@ -10,10 +10,13 @@
 //   * writes its value to `dense` (a value outside the band has the class of the exact one),
 //   * flags the ray dead when sdf <= -th - margin (certainly full: early termination),
 //   * flags the sample for the exact split-fp16 pass when |sdf| < th + margin.
-// The margin (ErtArgs.margin, default 0.02 = 2 th) bounds the lite pass's error: measured
-// max |lite - split-fp16| = 8.5e-4 over 1.8M in-ball samples of 18 shapes
-// (tools/cheap_error.py), i.e. a 24x safety factor; the refined samples then carry the
-// exact values, so every occupancy, mask and de_do downstream is the split-fp16 one.
+// The margin bounds the lite pass's error and calibrates itself per object: 0.02 in the
+// first GN iteration, then max(0.005, 8 x the largest |lite - exact| the object's own
+// re-decoded samples have shown so far) — the exact pass measures that error on every
+// band sample it overwrites (max 8.5e-4 over 1.8M samples of 18 shapes offline,
+// tools/cheap_error.py); a margin above 0.1 sends every sample to the exact pass.  The
+// refined samples carry the exact values, so every occupancy, mask and de_do downstream
+// is the split-fp16 one.
 // Layout: tile = 128 points, 512 threads; wave w owns rows 64w..64w+63 as 4 x 8 blocks of
 // 16x16 accumulators; LDS image H[128][528] fp16 (per-tile power-of-two scale as in
 // dsr_mlp16.hpp); weights: the hi pieces of the split fragments (one 1 KiB wave-load per
@@ -220,9 +223,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
       if (px != px || py != py || pz != pz || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
         y = __builtin_nanf("");
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
+      const float margin = E.st[tl.obj].lite_margin;
       dense[d.cand_off + idx] = y;
-      if (y <= E.nth - E.margin) E.dead[d.ray_off + idx / E.M] = 1;          // certainly full
-      else if (!(y >= -E.nth + E.margin)) E.refine[d.cand_off + idx] = 1;    // band (or NaN)
+      if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;            // certainly full
+      else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;      // band (or NaN)
     }
     __syncthreads();
   }

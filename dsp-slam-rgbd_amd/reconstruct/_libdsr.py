@@ -62,7 +62,7 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 3          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 4          # include/dsr.h DSR_ABI_VERSION
 
 
 class Stats(C.Structure):
@@ -70,7 +70,8 @@ class Stats(C.Structure):
                 ("fwd_points", C.c_int64), ("jac_points", C.c_int64),
                 ("fwd_launches", C.c_int), ("jac_launches", C.c_int), ("inball_points", C.c_int64),
                 ("lite", C.c_int), ("refine_launches", C.c_int), ("refine_ms", C.c_double),
-                ("refine_points", C.c_int64)]
+                ("refine_points", C.c_int64), ("lite_max_err", C.c_double),
+                ("lite_min_margin", C.c_double)]
 
 
 #: every function declared in include/dsr.h, with its ctypes signature

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 3
+#define DSR_ABI_VERSION 4
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -128,6 +128,8 @@ typedef struct {
   int refine_launches;
   double refine_ms;
   int64_t refine_points;
+  double lite_max_err;            /* max |lite - exact| over the re-decoded samples, all objects */
+  double lite_min_margin;         /* smallest classification margin the last run used */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */

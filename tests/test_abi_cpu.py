@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
                          text=True, check=True).stdout
     for f in fns:
         assert re.search(rf"\bT {f}$", out, flags=re.M), f
-    assert lib.dsr_abi_version() == 3
+    assert lib.dsr_abi_version() == 4
 
 
 STRUCTS = {"dsr_decoder_desc": "DecoderDesc", "dsr_optim_params": "OptimParams",

@@ -479,3 +479,45 @@ def test_graph_replay_bitwise(gpu_decoder, monkeypatch):
                 assert np.array_equal(s[0], sig[0][0]) and s[1:] == sig[0][1:]
         finally:
             lib.dsr_batch_destroy(h)
+
+
+def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
+    """The one-product classification pass + exact re-decode of the band (dsr_mlp_lite.hpp)
+    vs decoding every sample exactly (DSR_LITE=0): same N_valid, K and step; and the pass's
+    own error monitor stays far inside the margin it calibrates."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    f = golden("f4_traj_kitti0.npz")
+    one = dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=1))
+    opt = _opt(gpu_decoder, one, "KITTI")
+    n_it = int(f["n_iters_run"])
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
+            for e in range(n_it)]
+    out = {}
+    for lite in ("0", "1"):
+        monkeypatch.setenv("DSR_LITE", lite)
+        out[lite] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    (r0, t0), (r1, t1) = out["0"], out["1"]
+    for e in range(n_it):
+        assert r1[e]["is_good"] == r0[e]["is_good"]
+        assert int(t1[e]["n_valid"][0]) == int(t0[e]["n_valid"][0])
+        assert int(t1[e]["k"][0]) == int(t0[e]["k"][0]), e
+        assert abs(t1[e]["loss"][0] - t0[e]["loss"][0]) <= 1e-5 * abs(t0[e]["loss"][0])
+        assert rel(t1[e]["H"][0], t0[e]["H"][0]) <= 1e-4
+        assert step_err(t1[e]["dx"][0], t0[e]["dx"][0], t0[e]["H"][0]) <= 1e-3
+
+    monkeypatch.setenv("DSR_LITE", "1")
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
+    try:
+        ctx.check(lib.dsr_batch_run(h), "run")
+        st = L.Stats()
+        ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+    finally:
+        lib.dsr_batch_destroy(h)
+    assert st.lite == 1 and st.refine_points > 0 and st.refine_launches > 0
+    assert 0.0 < st.lite_max_err < 0.005 / 4           # 4x inside the smallest margin
+    assert abs(st.lite_min_margin - 0.005) < 1e-7      # floor reached after calibration
