@@ -36,7 +36,7 @@ struct dsr_ctx {
 // bit3 split-fp16, bit4 cross-layer A prefetch (split-fp16 only); 12 + 16*{2,4,8,16,24} are
 // timing experiments with invalid results: reduced / no epilogue, one MFMA product, no A streaming)
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
-                           const float*, float*, unsigned*, ErtArgs);
+                           const float*, float*, unsigned*, ErtArgs, MaskArgs);
 static FwdKernel fwd_kernel(int v) {
   switch (v & 15) {
     case 1: return k_mlp_fwd<1>;
@@ -60,7 +60,7 @@ static FwdKernel fwd_kernel(int v) {
 }
 using JacKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const ObjState*, const float*,
                            const float4*, const float*, const float*, const float*, GNParams, float*,
-                           const float4*, float*, float*);
+                           const float4*, float*, float*, MaskArgs);
 static int jac_variant();
 static JacKernel jac_kernel() {
   const int v = jac_variant();
@@ -114,6 +114,7 @@ struct dsr_batch {
   // kernels (objects never interact; every group owns its tile tables and counters).
   struct Group {
     int o0 = 0, n = 0;
+    int c0 = 0, c1 = 0;        // cand range of the group's objects
     Tile *tiles_f = nullptr, *tiles_j = nullptr;
     int *nt_f = nullptr, *nt_j = nullptr;
     unsigned* sync = nullptr;
@@ -128,6 +129,8 @@ struct dsr_batch {
   int* tr_i = nullptr;
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
   unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
+  MaskArgs ma{nullptr, nullptr, nullptr, nullptr};   // kept masks of the exact re-decode
+  int* kslot = nullptr;
   bool lite = true;             // lite classification pass + exact re-decode of the band
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
@@ -554,6 +557,14 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1);
   }
   if (b->lite) {
+    const char* km = getenv("DSR_KEEP_MASKS");
+    if (!(km && atoi(km) == 0)) {     // 512 B of masks per sample of the worst case: HBM is ample
+      ALLOC(b->ma.msk, sizeof(uint16_t) * 256 * (size_t)std::max(1, cand_off));
+      ALLOC(b->ma.yv, sizeof(float) * (size_t)std::max(1, cand_off));
+      ALLOC(b->ma.slotmap, sizeof(int) * (size_t)std::max(1, cand_off));
+      ALLOC(b->kslot, sizeof(int) * (size_t)std::max(1, cand_off));
+      b->ma.kslot = b->kslot;
+    }
     ALLOC(b->refine, (size_t)std::max(1, cand_off));
     if (hipMemset(b->refine, 0, (size_t)std::max(1, cand_off)) != hipSuccess) {
       dsr_batch_destroy(b);
@@ -564,6 +575,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
   ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
   for (auto& gr : b->groups) {
+    gr.c0 = b->hdesc[gr.o0].cand_off;
+    gr.c1 = b->hdesc[gr.o0 + gr.n - 1].cand_off + b->hdesc[gr.o0 + gr.n - 1].n_rays * M;
     size_t ft = 0, jt = 0;
     for (int o = gr.o0; o < gr.o0 + gr.n; ++o) { ft += ftile_o[o]; jt += jtile_o[o]; }
     ALLOC(gr.tiles_f, sizeof(Tile) * std::max<size_t>(1, ft));
@@ -728,30 +741,39 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
         if (b->lite)
-          hipLaunchKernelGGL(k_mlp_fwd_lite<true>, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+          hipLaunchKernelGGL((k_mlp_fwd_lite<true>), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
                              b->cand, b0, b4, b->dense, ert);
         else
           hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                             b0, b4, b->dense, gr.sync, ert);
+                             b0, b4, b->dense, gr.sync, ert, MaskArgs{nullptr, nullptr, nullptr, nullptr});
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
       }
       if (b->lite) {                             // exact split-fp16 decode of the band samples
+        if (b->ma.slotmap)
+          DSR_CHECK(ctx, hipMemsetAsync(b->ma.slotmap + gr.c0, 0xff, sizeof(int) * (size_t)(gr.c1 - gr.c0), s));
         hipLaunchKernelGGL(k_refine_compact, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->cand, b->refine);
+                           b->cand, b->refine, b->ma.slotmap);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
-        hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                           b0, b4, b->dense, gr.sync, ErtArgs{nullptr, b->M, -P.cut_off, st, nullptr});
+        const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
+        if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
+          hipLaunchKernelGGL((k_mlp_fwd16<true, 512>), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+                             b->cand, b0, b4, b->dense, gr.sync, ex, b->ma);
+        else
+          hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                             b0, b4, b->dense, gr.sync, ex, MaskArgs{nullptr, nullptr, nullptr, nullptr});
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
       }
+      const bool keep = b->lite && b->ma.msk && fv == 12;
       const int je = 2 * (np + (b->lite ? 1 : 0));
       hipLaunchKernelGGL(k_render, dim3(ng), dim3(RENDER_THREADS), 0, s, ng, desc, st, b->rays, b->dobs, P,
-                         b->dense, b->kpts, b->kres);
+                         b->dense, b->kpts, b->kres, (const int*)b->ma.slotmap, keep ? b->kslot : nullptr);
       hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
                          b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
-                         (const float4*)nullptr, (float*)nullptr, (float*)nullptr);
+                         (const float4*)nullptr, (float*)nullptr, (float*)nullptr,
+                         keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
       hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
                          b->counts + (size_t)o0 * 4, n);
@@ -996,7 +1018,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
-                     ErtArgs{nullptr, 1, 0.f, nullptr, nullptr});
+                     ErtArgs{nullptr, 1, 0.f, nullptr, nullptr}, MaskArgs{nullptr, nullptr, nullptr, nullptr});
   const int B = 256;
   hipLaunchKernelGGL(k_mc_edges, dim3((n + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->flag);
   hipLaunchKernelGGL(k_mc_cells, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->ntri);
@@ -1068,11 +1090,13 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
     hipLaunchKernelGGL(jac_kernel(), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const ObjState*)nullptr, (const float*)nullptr,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
-                       (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr);
+                       (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr,
+                       MaskArgs{nullptr, nullptr, nullptr, nullptr});
   } else {
     hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
-                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr});
+                       (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr},
+                       MaskArgs{nullptr, nullptr, nullptr, nullptr});
   }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
     cleanup();
@@ -1152,7 +1176,8 @@ int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* 
     hipLaunchKernelGGL(jac_kernel(), dim3(std::max(1, std::min(ctx->n_cu, nt))), dim3(512), 0, s, D, (const Tile*)dt,
                        (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst, (const float*)dpts,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
-                       (float*)dslots, (const float4*)nullptr, (float*)nullptr, filter ? (float*)dres : (float*)nullptr);
+                       (float*)dslots, (const float4*)nullptr, (float*)nullptr, filter ? (float*)dres : (float*)nullptr,
+                       MaskArgs{nullptr, nullptr, nullptr, nullptr});
     hipLaunchKernelGGL(k_solve_pose, dim3(1), dim3(256), 0, s, nt, n, (ObjState*)dst, (const float*)dslots);
     if (filter) {
       std::vector<float> res(n);

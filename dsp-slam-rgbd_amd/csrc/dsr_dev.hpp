@@ -99,6 +99,19 @@ struct ErtArgs {
   unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
 };
 
+// ReLU masks + SDF of the samples the exact pass re-decodes after the lite pass, so the
+// Jacobian kernel runs only the backward chain for render points (loss.py:157 re-forwards
+// them through autograd; the masks and tanh input are the same values).
+//   msk[slot][layer 0..7][wave 0..7][g 0..3]: 16 bits = rows 64w + 16q + 4g + r (bit 4q+r)
+//   yv[slot]: sdf; slotmap[sample] = slot (or -1); kslot[k] = slot of render point k
+// (slot, sample and k are offsets from the object's cand_off)
+struct MaskArgs {
+  uint16_t* msk;
+  float* yv;
+  int* slotmap;
+  const int* kslot;
+};
+
 struct GNParams {
   float k1, k2, k3, k4, b1, b2, lr, s_damp, cut_off;
   int iters, M;

@@ -366,7 +366,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
 __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, const ObjDesc* __restrict__ desc,
                                                                    ObjState* st, const float* __restrict__ rays_all,
                                                                    int M, float4* __restrict__ cand,
-                                                                   unsigned char* __restrict__ refine) {
+                                                                   unsigned char* __restrict__ refine,
+                                                                   int* __restrict__ slotmap) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -393,6 +394,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
     for (uint64_t m = bits; m; m &= m - 1) {
       const int j = __builtin_ctzll(m);
       const float3 x = ray_sample(rays, S, ray, j);
+      if (slotmap) slotmap[d.cand_off + ray * M + j] = off;
       cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
     }
     __syncthreads();
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
                                                  const float* __restrict__ bias0f,
                                                  const float* __restrict__ bias4f,
                                                  float* __restrict__ dense,
-                                                 unsigned* __restrict__ sync_ctr, ErtArgs E) {
+                                                 unsigned* __restrict__ sync_ctr, ErtArgs E, MaskArgs) {
   __shared__ FwdShared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -558,7 +560,9 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
                                                            const float* __restrict__ dobs_all, GNParams P,
                                                            const float* __restrict__ dense,
                                                            float4* __restrict__ kpts,
-                                                           float* __restrict__ kres) {
+                                                           float* __restrict__ kres,
+                                                           const int* __restrict__ slotmap,
+                                                           int* __restrict__ kslot) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -635,6 +639,7 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
         const float3 x = ray_sample(rays, S, ray, jj);
         kpts[d.cand_off + off] = make_float4(x.x, x.y, x.z, deds);
         kres[d.cand_off + off] = res;
+        if (kslot) kslot[d.cand_off + off] = slotmap[d.cand_off + ray * M + jj];
         ++off;
       }
     }
@@ -768,7 +773,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
                                                  float* __restrict__ slots,
                                                  const float4* __restrict__ raw_pts,
                                                  float* __restrict__ raw_out,
-                                                 float* __restrict__ res_out) {
+                                                 float* __restrict__ res_out, MaskArgs) {
   __shared__ JacShared sm;
   constexpr int JV = DSR_JAC_VARIANT;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -904,7 +909,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
                                                    float* __restrict__ slots,
                                                    const float4* __restrict__ raw_pts,
                                                    float* __restrict__ raw_out,
-                                                   float* __restrict__ res_out) {
+                                                   float* __restrict__ res_out, MaskArgs MA) {
   __shared__ Jac16Shared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -939,100 +944,134 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     __syncthreads();
     uint64_t mk[8];
     float v[4][4][4];
-    int sa;
-    // ---- lin0 (VALU, fp32) + masks
-    {
-      const float* bias0 = bias0f + tl.obj * HID;
-      float m = 0.f;
-      mk[0] = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n0 = 64 * w + 16 * q + 4 * g;
-        const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
-        float wx[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const int p = 16 * cb + c;
-          const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
-            const float h = fmaxf(a, 0.f);            // NaN re-imposed after the backward
-            if (h > 0.f) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
-            v[q][cb][r] = h;
-            m = fmaxf(m, fabsf(h));
-          }
-        }
-      }
-      sa = block_scale(m, sm.wmax, w, lane);
-      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
-    }
-    __syncthreads();
     floatx4 acc[4][4];
-    // ---- forward lin1..lin6 (masks kept)
-#pragma unroll 1
-    for (int l = 1; l <= 6; ++l) {
-      const int T = D.Kf[l] / 32;
-      if constexpr (XP) {
-        const int Tn = D.Kf[l + 1] / 32;
-        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                               wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
-      } else {
-        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
-      }
-      const float usc = ldexpf(1.f, -(D.sw[l] + sa));
-      const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
-      float m = 0.f;
-      mk[l] = 0;
+    int sa;
+    // render points whose ReLU masks and sdf the exact re-decode kept (MaskArgs): only the
+    // backward chain runs; otherwise the forward recomputes them (loss.py:157)
+    bool fast = false;
+    if (MA.kslot != nullptr && tl.term == 1) {
+      int bad = 0;
+      if (tid < tl.count) bad = MA.kslot[d.cand_off + tl.start + tid] < 0;
+      fast = !__syncthreads_or(bad);
+    }
+    if (fast) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n0 = 64 * w + 16 * q + 4 * g;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+      for (int l = 0; l < 8; ++l) mk[l] = 0;
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const int p = 16 * cb + c;
+      for (int cb = 0; cb < 4; ++cb) {
+        const int p = 16 * cb + c;
+        if (p < tl.count) {
+          const int slot = MA.kslot[d.cand_off + tl.start + p];
+          const uint16_t* src = MA.msk + (size_t)(d.cand_off + slot) * 256 + w * 4 + g;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
-            if (h > 0.f) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
-            if (l == 3 && n0 == 444 && r > 0) h = sm.xyz[p * 4 + (r - 1)];
-            v[q][cb][r] = h;
-            m = fmaxf(m, fabsf(h));
+          for (int l = 0; l < 8; ++l) {
+            const unsigned u = src[l * 32];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) mk[l] |= (uint64_t)((u >> (4 * q)) & 0xFu) << (16 * q + 4 * cb);
           }
         }
       }
-      sa = block_scale(m, sm.wmax, w, lane);
-      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      if (tid < TILE)
+        sm.y[tid] = (tid < tl.count) ? MA.yv[d.cand_off + MA.kslot[d.cand_off + tl.start + tid]] : 0.f;
+      if constexpr (XP) {                // the prefetched lin1 fragments are not needed: lin7^T
+        const int Tb = D.Kb[7] / 32;
+        load_a0<4>(wfrag(D.Wbh_raw[7], w, Tb), Tb, ah0, al0, lane);
+      }
+      __syncthreads();
+    } else {
+      // ---- lin0 (VALU, fp32) + masks
+      {
+        const float* bias0 = bias0f + tl.obj * HID;
+        float m = 0.f;
+        mk[0] = 0;
+  #pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n0 = 64 * w + 16 * q + 4 * g;
+          const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
+          float wx[12];
+  #pragma unroll
+          for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
+  #pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            const int p = 16 * cb + c;
+            const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+              const float h = fmaxf(a, 0.f);            // NaN re-imposed after the backward
+              if (h > 0.f) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
+              v[q][cb][r] = h;
+              m = fmaxf(m, fabsf(h));
+            }
+          }
+        }
+        sa = block_scale(m, sm.wmax, w, lane);
+        write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      }
+      __syncthreads();
+      // ---- forward lin1..lin6 (masks kept)
+  #pragma unroll 1
+      for (int l = 1; l <= 6; ++l) {
+        const int T = D.Kf[l] / 32;
+        if constexpr (XP) {
+          const int Tn = D.Kf[l + 1] / 32;
+          gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                                 wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
+        } else {
+          gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
+        }
+        const float usc = ldexpf(1.f, -(D.sw[l] + sa));
+        const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
+        float m = 0.f;
+        mk[l] = 0;
+  #pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n0 = 64 * w + 16 * q + 4 * g;
+          const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+  #pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            const int p = 16 * cb + c;
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+              if (h > 0.f) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
+              if (l == 3 && n0 == 444 && r > 0) h = sm.xyz[p * 4 + (r - 1)];
+              v[q][cb][r] = h;
+              m = fmaxf(m, fabsf(h));
+            }
+          }
+        }
+        sa = block_scale(m, sm.wmax, w, lane);
+        write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+        __syncthreads();
+      }
+      // ---- lin7 + lin8 dot + tanh
+      {
+        const int T = D.Kf[7] / 32;
+        if constexpr (XP) {
+          const int Tn = D.Kb[7] / 32;
+          gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
+                                 wfrag(D.Wbh_raw[7], w, Tn), Tn);
+        } else {
+          gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
+        }
+        const int un = D.sw[7] + sa;
+  #pragma unroll
+        for (int q = 0; q < 4; ++q)
+  #pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
+        epi_l7(acc, D, sm.red, w, lane, mk[7]);
+      }
+      __syncthreads();
+      if (tid < TILE) {
+        float s = sm.red[tid];
+        for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+        sm.y[tid] = tanhf(s + D.b8);
+      }
       __syncthreads();
     }
-    // ---- lin7 + lin8 dot + tanh
-    {
-      const int T = D.Kf[7] / 32;
-      if constexpr (XP) {
-        const int Tn = D.Kb[7] / 32;
-        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                               wfrag(D.Wbh_raw[7], w, Tn), Tn);
-      } else {
-        gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
-      }
-      const int un = D.sw[7] + sa;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
-      epi_l7(acc, D, sm.red, w, lane, mk[7]);
-    }
-    __syncthreads();
-    if (tid < TILE) {
-      float s = sm.red[tid];
-      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
-      sm.y[tid] = tanhf(s + D.b8);
-    }
-    __syncthreads();
     // ---- g7 = (1 - y^2) W8 (.) relu'(a7)
     {
       float m = 0.f;

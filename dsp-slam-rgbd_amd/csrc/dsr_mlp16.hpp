@@ -230,12 +230,40 @@ __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _F
 
 // Shared epilogue: v = relu(acc * 2^-unscale + bias) (+ xyz rows for lin3), block max,
 // one barrier, scale, split-write.  Returns the new activation scale exponent.
+// 16-bit lane slices of a layer's ReLU mask (bit (q*4+cb)*4+r of mk, the Jacobian kernel's
+// layout) for the lane's 4 points, stored per sample as MaskArgs.msk
+__device__ __forceinline__ void store_mask16(uint64_t mk, uint16_t* msk, int cand_base, int count, int l,
+                                             int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int p = 16 * cb + c;
+    unsigned u = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u |= (unsigned)((mk >> (16 * q + 4 * cb)) & 0xFull) << (4 * q);
+    if (p < count) msk[(size_t)(cand_base + p) * 256 + l * 32 + w * 4 + g] = (uint16_t)u;
+  }
+}
+
+__device__ __forceinline__ uint64_t relu_bits(const float (&v)[4][4][4]) {
+  uint64_t mk = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (v[q][cb][r] > 0.f) mk |= 1ull << ((q * 4 + cb) * 4 + r);
+  return mk;
+}
+
 __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
-                                     Fwd16Shared& sm, int w, int lane, bool is_l3) {
+                                     Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
   float m = 0.f;
+  uint64_t bits = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n0 = 64 * w + 16 * q + 4 * g;
@@ -248,6 +276,7 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
         // acc*2^-unscale is exact, so the fma rounds exactly like (acc*2^-un) + b; ReLU as
         // v_max (NaN inputs are re-imposed on the output, see nan_in below)
         float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+        if (x > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
         if (is_l3 && n0 == 444 && r > 0) x = sm.xyz[p * 4 + (r - 1)];
         v[q][cb][r] = x;
         m = fmaxf(m, x);                  // x >= 0
@@ -262,6 +291,7 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
   for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
   const int s = act_scale_exp(mm);
   write_split(v, s, sm.Hh, sm.Hl, w, lane);
+  mk = bits;
   return s;
 }
 
@@ -275,7 +305,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
                                                    const float* __restrict__ bias0f,
                                                    const float* __restrict__ bias4f,
                                                    float* __restrict__ dense, unsigned* __restrict__,
-                                                   ErtArgs E) {
+                                                   ErtArgs E, MaskArgs MA) {
   __shared__ Fwd16Shared sm;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -284,6 +314,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   constexpr bool XP = (X & 1) != 0;
   constexpr int EXPM = X & 6;
   constexpr int EX = (X >> 3) & 3;
+  constexpr bool MSK = (X & 512) != 0;     // exact re-decode: keep masks + sdf (MaskArgs)
   const int T1 = D.Kf[1] / 32;
   half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
   if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
@@ -329,6 +360,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
       sa = act_scale_exp(mm);
       write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      if constexpr (MSK) store_mask16(relu_bits(v), MA.msk, d.cand_off + tl.start, tl.count, 0, w, lane);
     }
     __syncthreads();
     floatx4 acc[4][4];
@@ -342,7 +374,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         gemm16_tile<PRIO, 4, EX>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
       }
       if constexpr (EXPM == 0) {
-        sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3);
+        uint64_t mk;
+        sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
+        if constexpr (MSK) store_mask16(mk, MA.msk, d.cand_off + tl.start, tl.count, l, w, lane);
       } else if constexpr (EXPM == 2) {
         __syncthreads();
 #pragma unroll
@@ -373,6 +407,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
       uint64_t mask;
       epi_l7(acc, D, sm.red, w, lane, mask);
+      if constexpr (MSK) store_mask16(mask, MA.msk, d.cand_off + tl.start, tl.count, 7, w, lane);
     }
     __syncthreads();
     if (tid < tl.count) {
@@ -390,6 +425,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
       }
       dense[d.cand_off + idx] = y;
+      if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
       if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
     }
     __syncthreads();

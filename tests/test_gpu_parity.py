@@ -497,17 +497,22 @@ def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
     objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
             for e in range(n_it)]
     out = {}
-    for lite in ("0", "1"):
+    # exact decode | lite + exact band, Jacobian re-forwards render points | ... masks kept
+    for lite, keep in (("0", "1"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("DSR_LITE", lite)
-        out[lite] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
-    (r0, t0), (r1, t1) = out["0"], out["1"]
-    for e in range(n_it):
-        assert r1[e]["is_good"] == r0[e]["is_good"]
-        assert int(t1[e]["n_valid"][0]) == int(t0[e]["n_valid"][0])
-        assert int(t1[e]["k"][0]) == int(t0[e]["k"][0]), e
-        assert abs(t1[e]["loss"][0] - t0[e]["loss"][0]) <= 1e-5 * abs(t0[e]["loss"][0])
-        assert rel(t1[e]["H"][0], t0[e]["H"][0]) <= 1e-4
-        assert step_err(t1[e]["dx"][0], t0[e]["dx"][0], t0[e]["H"][0]) <= 1e-3
+        monkeypatch.setenv("DSR_KEEP_MASKS", keep)
+        out[lite + keep] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    r0, t0 = out["01"]
+    for key in ("10", "11"):
+        r1, t1 = out[key]
+        for e in range(n_it):
+            assert r1[e]["is_good"] == r0[e]["is_good"]
+            assert int(t1[e]["n_valid"][0]) == int(t0[e]["n_valid"][0])
+            assert int(t1[e]["k"][0]) == int(t0[e]["k"][0]), (key, e)
+            assert abs(t1[e]["loss"][0] - t0[e]["loss"][0]) <= 1e-5 * abs(t0[e]["loss"][0])
+            assert rel(t1[e]["H"][0], t0[e]["H"][0]) <= 1e-4, (key, e)
+            assert step_err(t1[e]["dx"][0], t0[e]["dx"][0], t0[e]["H"][0]) <= 1e-3, (key, e)
+    monkeypatch.delenv("DSR_KEEP_MASKS")
 
     monkeypatch.setenv("DSR_LITE", "1")
     lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
