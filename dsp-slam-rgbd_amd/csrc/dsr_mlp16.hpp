@@ -279,7 +279,7 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
         if (x > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
         if (is_l3 && n0 == 444 && r > 0) x = sm.xyz[p * 4 + (r - 1)];
         v[q][cb][r] = x;
-        m = fmaxf(m, x);                  // x >= 0
+        m = fmaxf(m, fabsf(x));           // (xyz rows of lin3 may be negative)
       }
     }
   }

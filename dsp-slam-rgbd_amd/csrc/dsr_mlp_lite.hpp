@@ -177,7 +177,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
             float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
             if (l == 3 && n0 == 444 && r > 0) x = sm.xyz[(16 * cb + c) * 4 + (r - 1)];   // lin4 input: h3 | xyz
             acc[q][cb][r] = x;
-            m = fmaxf(m, x);
+            m = fmaxf(m, fabsf(x));           // (xyz rows of lin3 may be negative)
           }
         }
       }
