@@ -1308,23 +1308,38 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     }
     __syncthreads();
   }
-  if (tid < NPAR) {                     // column tid of inverse(H)
-    const int col = tid;
-    float x[NPAR];
-    for (int i = 0; i < NPAR; ++i) x[i] = (i == col) ? 1.f : 0.f;
+  // inverse(H) = U^-1 L^-1 P I, all 71 columns at once in LDS: the row permutation of
+  // the identity, then right-looking substitutions (one barrier per pivot row, every
+  // (row, column) pair in parallel; each element accumulates in the column-solve order)
+  for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) X[e / NPAR][e % NPAR] = 0.f;
+  __syncthreads();
+  if (tid == 0) {
+    int perm[NPAR];                       // P applied to the row indices of I
+    for (int i = 0; i < NPAR; ++i) perm[i] = i;
     for (int k = 0; k < NPAR; ++k) {
       const int p = piv[k];
-      if (p != k) { float t = x[k]; x[k] = x[p]; x[p] = t; }
+      if (p != k) { const int t = perm[k]; perm[k] = perm[p]; perm[p] = t; }
     }
-    for (int i = 0; i < NPAR; ++i)
-      for (int l = 0; l < i; ++l) x[i] = __builtin_fmaf(-A[i][l], x[l], x[i]);
-    for (int i = NPAR - 1; i >= 0; --i) {
-      for (int l = i + 1; l < NPAR; ++l) x[i] = __builtin_fmaf(-A[i][l], x[l], x[i]);
-      x[i] = x[i] / A[i][i];
-    }
-    for (int i = 0; i < NPAR; ++i) X[i][col] = x[i];
+    for (int i = 0; i < NPAR; ++i) X[i][perm[i]] = 1.f;
   }
   __syncthreads();
+  for (int l = 0; l < NPAR - 1; ++l) {    // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
+    const int m = NPAR - 1 - l;
+    for (int e = tid; e < m * NPAR; e += SOLVE_THREADS) {
+      const int i = l + 1 + e / NPAR, c = e % NPAR;
+      X[i][c] = __builtin_fmaf(-A[i][l], X[l][c], X[i][c]);
+    }
+    __syncthreads();
+  }
+  for (int i = NPAR - 1; i >= 0; --i) {   // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
+    for (int c = tid; c < NPAR; c += SOLVE_THREADS) X[i][c] = X[i][c] / A[i][i];
+    __syncthreads();
+    for (int e = tid; e < i * NPAR; e += SOLVE_THREADS) {
+      const int r = e / NPAR, c = e % NPAR;
+      X[r][c] = __builtin_fmaf(-A[r][i], X[i][c], X[r][c]);
+    }
+    __syncthreads();
+  }
   if (tid < NPAR) {                     // dx = inverse(H) b
     float s = 0.f;
     for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
