@@ -158,7 +158,17 @@ def test_trajectory_shadowing_and_final(gpu_decoder, oracle_dec, name, optim, dt
         tro, _, _ = O.gn_step(oracle_dec, P, state_T, z, f["obj_pts"], f["obj_rays"], dobs, n_fg)
         assert abs(tg["k"][0] - tro.k) <= 2
         assert abs(int(tg["n_valid"][0]) - tro.n_valid) <= 2
-        assert abs(tg["loss"][0] - tro.loss) <= 1e-4 * abs(tro.loss)
+        # terms separately, as in the teacher-forced test: the sdf term carries only fp32
+        # decoder noise; the render term additionally moves by <= 0.09/K per render point
+        # that flips across |sdf| = th or de_do = 1e-2 (clamp +-0.30, loss.py:147-148) — a
+        # flip can swap points without changing K, so allow up to 2 of them
+        jo = optim["joint_optim"]
+        assert abs(tg["sdf_loss"][0] - tro.sdf_loss) <= 5e-5 * abs(tro.sdf_loss)
+        flips = max(abs(int(tg["k"][0]) - tro.k), 2)
+        assert abs(tg["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
+                                                              + flips * 0.09 / tro.k), (e, tg["k"][0], tro.k)
+        assert abs(tg["loss"][0] - tro.loss) <= (1e-4 * abs(tro.loss)
+                                                 + jo["k1"] * flips * 0.09 / tro.k)
         assert rel(tg["H"][0], tro.H) <= 5e-3
         assert step_err(tg["dx"][0], tro.dx, tro.H) <= 2e-2
     assert np.isfinite(t["loss"]).all()
