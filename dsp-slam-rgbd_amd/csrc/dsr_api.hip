@@ -72,6 +72,25 @@ static JacKernel jac_kernel() {
   }
   return k_mlp_jac;
 }
+// Lite-pass variant (DSR_LITE_VARIANT, dsr_mlp_lite.hpp: lite_gemm): 16/32/48 = A ring of
+// 2/3/4 k steps, +8 static activation scale; 18 is a timing experiment (no A streaming)
+using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
+                            const float*, float*, ErtArgs);
+#ifndef DSR_DEFAULT_LITE_VARIANT
+#define DSR_DEFAULT_LITE_VARIANT 24
+#endif
+static LiteKernel lite_kernel() {
+  const char* e = getenv("DSR_LITE_VARIANT");
+  switch (e ? atoi(e) : DSR_DEFAULT_LITE_VARIANT) {
+    case 18: return k_mlp_fwd_lite<true, 18>;
+    case 16: return k_mlp_fwd_lite<true, 16>;
+    case 32: return k_mlp_fwd_lite<true, 32>;
+    case 40: return k_mlp_fwd_lite<true, 40>;
+    case 48: return k_mlp_fwd_lite<true, 48>;
+    case 56: return k_mlp_fwd_lite<true, 56>;
+  }
+  return k_mlp_fwd_lite<true, 24>;
+}
 static int fwd_variant() {
   const char* e = getenv("DSR_FWD_VARIANT");
   return e ? atoi(e) : DSR_DEFAULT_FWD_VARIANT;
@@ -713,6 +732,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
   const int fv = fwd_variant();
   const FwdKernel fwdk = fwd_kernel(fv);
   const JacKernel jack = jac_kernel();
+  const LiteKernel litek = lite_kernel();
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
@@ -741,7 +761,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
         if (b->lite)
-          hipLaunchKernelGGL((k_mlp_fwd_lite<true>), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+          hipLaunchKernelGGL(litek, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
                              b->cand, b0, b4, b->dense, ert);
         else
           hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,

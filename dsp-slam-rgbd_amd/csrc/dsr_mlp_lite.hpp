@@ -18,10 +18,19 @@
 // refined samples carry the exact values, so every occupancy, mask and de_do downstream
 // is the split-fp16 one.
 // Layout: tile = 128 points, 512 threads; wave w owns rows 64w..64w+63 as 4 x 8 blocks of
-// 16x16 accumulators; LDS image H[128][528] fp16 (per-tile power-of-two scale as in
-// dsr_mlp16.hpp); weights: the hi pieces of the split fragments (one 1 KiB wave-load per
-// row block and k step).
+// 16x16 accumulators; LDS image H[128][528] fp16; weights: the hi pieces of the split
+// fragments (one 1 KiB wave-load per row block and k step), streamed from L2 through a ring
+// of NB k steps in flight (gemm_lite).
+//
+// Register discipline.  The accumulators take 128 of the wave's 256 VGPRs, so every other
+// value live across a GEMM costs ring depth.  Lane-derived values (LDS addresses, shuffle
+// indices, bias offsets) are re-derived per layer from an opaque copy of the lane id
+// (`opaque`), so the compiler cannot hoist them out of the tile loop and keep ~60 of them
+// live through every GEMM (which it otherwise does).  Conditions that single out rows
+// (lin4's xyz rows) are split into a wave-uniform branch + a per-lane select, never a
+// per-element divergent branch.
 #pragma once
+#include <utility>
 #include "dsr_dev.hpp"
 #include "dsr_mlp.hpp"
 #include "dsr_mlp16.hpp"
@@ -35,60 +44,102 @@ struct LiteShared {
   float xyz[LTILE * 4];
   float red[NWAVE * LTILE];
   float wmax[NWAVE];
+  int ovf;
 };
 
-// acc[4][8] = hi(A rows of this wave) . hi(H) over K = 32*T
-template <bool PRIO>
-__device__ __forceinline__ void gemm_lite(const half8* __restrict__ A, int T, const _Float16* H,
-                                          floatx4 (&acc)[4][8], int lane) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+// acc[4][8] = hi(A rows of this wave) . hi(H) over K = 32*T.
+// Ring schedule: NB A-fragment sets in flight (the loads for k step t+NB-1 issue as step t
+// starts, into the set step t-1 released), buffer loads (one wave-uniform descriptor per
+// layer slice, the lane's 16-byte offset in one VGPR, the (q, k step) offset in an SGPR), and
+// a 4-deep B ring: the B fragment of column block cb+3 (of this step or, past the last block,
+// of the next one) is read from LDS as the MFMAs of block cb issue, so 4 B fragments are live.
+// The first step starts the accumulators from an inline zero C operand.
+// LV bit1 (timing experiment, invalid results): every step re-reads step 0's A fragments.
+template <bool PRIO, int T, int NB, int LV>
+__device__ __forceinline__ void gemm_lite(const _Float16* Wl, int w, const _Float16* H, floatx4 (&acc)[4][8],
+                                          int lane) {
+  const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
+  const int voff = lane * 16;
   const _Float16* B = H + (lane & 15) * PH + 8 * (lane >> 4);
-  half8 a0[4], a1[4], b0[8], b1[8];
+  auto lda = [&](int q, int t) {
+    const int so = ((LV & 2) ? q * T : q * T + t) * 2048;
+    return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0));
+  };
+  auto ldb = [&](int cb, int k32) { return *reinterpret_cast<const half8*>(B + cb * 16 * PH + k32); };
+  half8 a[NB][4], b[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) a0[q] = A[((q * T) * 2) * 64 + lane];
+  for (int j = 0; j < NB - 1; ++j)
 #pragma unroll
-  for (int cb = 0; cb < 8; ++cb) b0[cb] = *reinterpret_cast<const half8*>(B + cb * 16 * PH);
-  for (int t = 0; t < T; t += 2) {
+    for (int q = 0; q < 4; ++q) a[j][q] = lda(q, j);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a1[q] = A[((q * T + t + 1) * 2) * 64 + lane];
+  for (int cb = 0; cb < 3; ++cb) b[cb] = ldb(cb, 0);
+  // step t uses ring slot J = t % NB
+  auto step = [&](auto J, auto FIRST, int t) {
+    constexpr int j = decltype(J)::value;
+    if (t + NB - 1 < T) {
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) b1[cb] = *reinterpret_cast<const half8*>(B + cb * 16 * PH + 32 * (t + 1));
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb)
-        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[q], b0[cb], acc[q][cb], 0, 0, 0);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-    if (t + 2 < T) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a0[q] = A[((q * T + t + 2) * 2) * 64 + lane];
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) b0[cb] = *reinterpret_cast<const half8*>(B + cb * 16 * PH + 32 * (t + 2));
+      for (int q = 0; q < 4; ++q) a[(j + NB - 1) % NB][q] = lda(q, t + NB - 1);
     }
+    const int pc = 32 * t, pn = 32 * (t + 1);   // (k step T: columns 512.. of the 528 pitch, unused)
     if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int cb = 0; cb < 8; ++cb) {
+      b[(cb + 3) & 3] = (cb + 3 < 8) ? ldb(cb + 3, pc) : ldb(cb - 5, pn);
 #pragma unroll
-      for (int cb = 0; cb < 8; ++cb)
-        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[q], b1[cb], acc[q][cb], 0, 0, 0);
+      for (int q = 0; q < 4; ++q)
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+            a[j][q], b[cb & 3], decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb], 0, 0, 0);
+    }
     if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  step(std::integral_constant<int, 0>{}, std::true_type{}, 0);
+  constexpr int TM = 1 + (T - 1) / NB * NB;     // steps 1 .. TM-1 in groups of NB, then the rest
+#pragma unroll 1
+  for (int t0 = 1; t0 < TM; t0 += NB) {
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      (step(std::integral_constant<int, (1 + J) % NB>{}, std::false_type{}, t0 + J), ...);
+    }(std::make_integer_sequence<int, NB>{});
   }
+  [&]<int... J>(std::integer_sequence<int, J...>) {
+    (step(std::integral_constant<int, (TM + J) % NB>{}, std::false_type{}, TM + J), ...);
+  }(std::make_integer_sequence<int, T - TM>{});
 }
 
-// block max of m (>= 0) -> power-of-two scale exponent; contains the barrier that ends
-// every wave's reads of H for the GEMM just finished
-__device__ __forceinline__ int lite_block_scale(float m, float* wmax, int w, int lane) {
-  m = wave_max(m);
-  if (lane == 0) wmax[w] = m;
-  __syncthreads();
-  float mm = wmax[0];
+// LV (DSR_LITE_VARIANT): bits 4-5 = NB - 1 (ring depth; 0 is read as NB 2), bit3 static
+// activation scale (lite_scale), bit1 timing experiment (no A streaming).
+template <bool PRIO, int LV>
+__device__ __forceinline__ void lite_gemm(const _Float16* Wl, int w, int T, const _Float16* H,
+                                          floatx4 (&acc)[4][8], int lane) {
+  constexpr int NB = ((LV >> 4) & 3) == 0 ? 2 : 1 + ((LV >> 4) & 3);
+  if (T != 14) gemm_lite<PRIO, 16, NB, LV>(Wl, w, H, acc, lane);   // K 512
+  else gemm_lite<PRIO, 14, NB, LV>(Wl, w, H, acc, lane);           // K 448 (lin4: h3 | xyz)
+}
+
+// Per-tile activation scale exponent; contains the barrier that ends every wave's reads of H
+// for the GEMM just finished.
+// Default: block max of m (>= 0) -> power of two (act_scale_exp).
+// LV bit3: static scale 2^0 — fp16 keeps 11 significant bits over 6e-5..65504 whatever the
+// tile's max, so the block max only guards the range: no max exchange and no rescale
+// multiply; a tile whose activations reach 2^15 sets `ovf` and all its samples go to the
+// exact pass instead (so the lite pass can never misclassify through an overflow).
+template <int LV>
+__device__ __forceinline__ int lite_scale(float m, float* wmax, int* ovf, int w, int lane) {
+  if constexpr ((LV & 8) != 0) {
+    if (!(m < 32768.f)) *ovf = 1;
+    __syncthreads();
+    return 0;
+  } else {
 #pragma unroll
-  for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, wmax[k]);
-  return act_scale_exp(mm);
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, xor_lane(m, lane, o));
+    if (lane == 0) wmax[w] = m;
+    __syncthreads();
+    float mm = wmax[0];
+#pragma unroll
+    for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, wmax[k]);
+    return act_scale_exp(mm);
+  }
 }
 
 __device__ __forceinline__ void lite_write(floatx4 (&acc)[4][8], int s, _Float16* H, int w, int lane) {
@@ -107,7 +158,7 @@ __device__ __forceinline__ void lite_write(floatx4 (&acc)[4][8], int s, _Float16
   }
 }
 
-template <bool PRIO>
+template <bool PRIO, int LV = 16>
 __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* __restrict__ tiles,
                                                       const int* __restrict__ n_tiles,
                                                       const ObjDesc* __restrict__ desc,
@@ -116,23 +167,25 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
                                                       const float* __restrict__ bias4f,
                                                       float* __restrict__ dense, ErtArgs E) {
   __shared__ LiteShared sm;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
-    if (tid < LTILE) {
-      const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-      sm.xyz[tid * 4 + 0] = v.x; sm.xyz[tid * 4 + 1] = v.y;
-      sm.xyz[tid * 4 + 2] = v.z; sm.xyz[tid * 4 + 3] = v.w;
+    {
+      const int tid = opaque(threadIdx.x);
+      if (tid < LTILE) {
+        const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(sm.xyz + tid * 4) = v;
+      }
+      if (tid == 0) sm.ovf = 0;
     }
     __syncthreads();
     floatx4 acc[4][8];
     int sa;
     // ---- lin0 (3 inputs, fp32 VALU) into the accumulator layout
     {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       const float* bias0 = bias0f + tl.obj * HID;
       float m = 0.f;
 #pragma unroll
@@ -144,51 +197,60 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
         for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
 #pragma unroll
         for (int cb = 0; cb < 8; ++cb) {
-          const int p = 16 * cb + c;
-          const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
+          const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+            const float a = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
             const float h = fmaxf(a, 0.f);
             acc[q][cb][r] = h;
             m = fmaxf(m, h);
           }
         }
       }
-      sa = lite_block_scale(m, sm.wmax, w, lane);
+      sa = lite_scale<LV>(m, sm.wmax, &sm.ovf, w, lane);
       lite_write(acc, sa, sm.H, w, lane);
     }
     __syncthreads();
     // ---- lin1..lin6
+#pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
-      const int T = D.Kf[l] / 32;
-      gemm_lite<PRIO>(wfrag(D.Wh_raw[l], w, T), T, sm.H, acc, lane);
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      lite_gemm<PRIO, LV>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.H, acc, lane);
       const float usc = ldexpf(1.f, -(D.sw[l] + sa));
       const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
       float m = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int n0 = 64 * w + 16 * q + 4 * g;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+        const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
 #pragma unroll
         for (int cb = 0; cb < 8; ++cb) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
-            if (l == 3 && n0 == 444 && r > 0) x = sm.xyz[(16 * cb + c) * 4 + (r - 1)];   // lin4 input: h3 | xyz
+            const float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
             acc[q][cb][r] = x;
-            m = fmaxf(m, fabsf(x));           // (xyz rows of lin3 may be negative)
+            m = fmaxf(m, x);
           }
         }
       }
-      sa = lite_block_scale(m, sm.wmax, w, lane);
+      if (l == 3 && w == 6) {   // lin4 input = h3 | xyz: rows 445..447 (q 3, g 3, r 1..3) <- x, y, z
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+          const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
+          const bool on = g == 3;
+          acc[3][cb][1] = on ? p.x : acc[3][cb][1];
+          acc[3][cb][2] = on ? p.y : acc[3][cb][2];
+          acc[3][cb][3] = on ? p.z : acc[3][cb][3];
+          m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+        }
+      }
+      sa = lite_scale<LV>(m, sm.wmax, &sm.ovf, w, lane);
       lite_write(acc, sa, sm.H, w, lane);
       __syncthreads();
     }
     // ---- lin7 + relu, lin8 dot product, tanh
     {
-      const int T = D.Kf[7] / 32;
-      gemm_lite<PRIO>(wfrag(D.Wh_raw[7], w, T), T, sm.H, acc, lane);
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      lite_gemm<PRIO, LV>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.H, acc, lane);
       const float usc = ldexpf(1.f, -(D.sw[7] + sa));
       float part[8];
 #pragma unroll
@@ -209,24 +271,28 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) {
         float s = part[cb];
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
+        s += xor_lane(s, lane, 16);
+        s += xor_lane(s, lane, 32);
         if (g == 0) sm.red[w * LTILE + 16 * cb + c] = s;
       }
     }
     __syncthreads();
-    if (tid < tl.count) {
-      float s = sm.red[tid];
-      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * LTILE + tid];
-      float y = tanhf(s + D.b8);
-      const float px = sm.xyz[tid * 4 + 0], py = sm.xyz[tid * 4 + 1], pz = sm.xyz[tid * 4 + 2];
-      if (px != px || py != py || pz != pz || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
-        y = __builtin_nanf("");
-      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
-      const float margin = E.st[tl.obj].lite_margin;
-      dense[d.cand_off + idx] = y;
-      if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;            // certainly full
-      else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;      // band (or NaN)
+    {
+      const int tid = opaque(threadIdx.x);
+      if (tid < tl.count) {
+        float s = sm.red[tid];
+        for (int k = 1; k < NWAVE; ++k) s += sm.red[k * LTILE + tid];
+        float y = tanhf(s + D.b8);
+        const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
+        if (p.x != p.x || p.y != p.y || p.z != p.z || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
+          y = __builtin_nanf("");
+        const int idx = __float_as_int(p.w);
+        const float margin = E.st[tl.obj].lite_margin;
+        dense[d.cand_off + idx] = y;
+        if ((LV & 8) && sm.ovf) E.refine[d.cand_off + idx] = 1;                   // range guard
+        else if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;            // certainly full
+        else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;          // band (or NaN)
+      }
     }
     __syncthreads();
   }
