@@ -32,11 +32,29 @@ struct dsr_ctx {
   std::string err;
 };
 
-// Forward-kernel variant (DSR_FWD_VARIANT, bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
-// bit3 split-fp16, bit4 cross-layer A prefetch (split-fp16 only); 12 + 16*{2,4,8,16,24} are
-// timing experiments with invalid results: reduced / no epilogue, one MFMA product, no A streaming)
+// Forward-kernel variant (DSR_FWD_VARIANT: bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
+// bit3 split-fp16; 12 = split-fp16 + setprio, the default) and the A-ring depth of the split
+// kernels (DSR_SPLIT_RING: 0 = the two-set gemm16_tile, 2..4 = gemm16_ring k steps in flight)
+#ifndef DSR_DEFAULT_SPLIT_RING
+#define DSR_DEFAULT_SPLIT_RING 2
+#endif
+static int split_ring() {
+  const char* e = getenv("DSR_SPLIT_RING");
+  const int r = e ? atoi(e) : DSR_DEFAULT_SPLIT_RING;
+  return (r >= 2 && r <= 4) ? r : 0;
+}
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                            const float*, float*, unsigned*, ErtArgs, MaskArgs);
+// split-fp16 forward with X's mask bit (512) and the ring depth in bits 10-11
+template <int MSK>
+static FwdKernel fwd16_kernel() {
+  switch (split_ring()) {
+    case 2: return k_mlp_fwd16<true, MSK | 1024>;
+    case 3: return k_mlp_fwd16<true, MSK | 2048>;
+    case 4: return k_mlp_fwd16<true, MSK | 3072>;
+  }
+  return k_mlp_fwd16<true, MSK>;
+}
 static FwdKernel fwd_kernel(int v) {
   switch (v & 15) {
     case 1: return k_mlp_fwd<1>;
@@ -44,17 +62,8 @@ static FwdKernel fwd_kernel(int v) {
     case 3: return k_mlp_fwd<3>;
     case 6: return k_mlp_fwd<6>;
     case 7: return k_mlp_fwd<7>;
-    case 8: return (v & 16) ? k_mlp_fwd16<false, 1> : k_mlp_fwd16<false, 0>;
-    case 12:
-      switch (v >> 4) {       // bit4 cross-layer prefetch; bits 5-6 timing experiments
-        case 1: return k_mlp_fwd16<true, 1>;
-        case 2: return k_mlp_fwd16<true, 2>;
-        case 4: return k_mlp_fwd16<true, 4>;
-        case 8: return k_mlp_fwd16<true, 8>;       // 1 product
-        case 16: return k_mlp_fwd16<true, 16>;     // no A streaming
-        case 24: return k_mlp_fwd16<true, 24>;     // both
-        default: return k_mlp_fwd16<true, 0>;
-      }
+    case 8: return k_mlp_fwd16<false, 0>;
+    case 12: return fwd16_kernel<0>();
     default: return k_mlp_fwd<0>;
   }
 }
@@ -65,10 +74,14 @@ static int jac_variant();
 static JacKernel jac_kernel() {
   const int v = jac_variant();
   switch (v) {
-    case 8: return k_mlp_jac16<false, false>;
-    case 12: return k_mlp_jac16<true, false>;
-    case 24: return k_mlp_jac16<false, true>;
-    case 28: return k_mlp_jac16<true, true>;
+    case 8: return k_mlp_jac16<false, 0>;
+    case 12:
+      switch (split_ring()) {
+        case 2: return k_mlp_jac16<true, 2>;
+        case 3: return k_mlp_jac16<true, 3>;
+        case 4: return k_mlp_jac16<true, 4>;
+      }
+      return k_mlp_jac16<true, 0>;
   }
   return k_mlp_jac;
 }
@@ -672,7 +685,7 @@ static bool graph_enabled() {        // DSR_GRAPH=1: replay re-run batches as hi
   const char* ge = getenv("DSR_GRAPH");
   return ge && atoi(ge) != 0;
 }
-static long graph_key() { return (long)fwd_variant() * 100000 + jac_variant(); }
+static long graph_key() { return ((long)fwd_variant() * 100000 + jac_variant()) * 10 + split_ring(); }
 
 static int batch_capture(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
@@ -777,7 +790,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
         if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
-          hipLaunchKernelGGL((k_mlp_fwd16<true, 512>), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+          hipLaunchKernelGGL(fwd16_kernel<512>(), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
                              b->cand, b0, b4, b->dense, gr.sync, ex, b->ma);
         else
           hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,

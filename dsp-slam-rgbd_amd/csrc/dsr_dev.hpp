@@ -125,4 +125,17 @@ __device__ __forceinline__ float fetch4(const float4& v, int j) {
   return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
 
+// x, re-materialised at this point: the compiler may not assume it equals an earlier x, so
+// values derived from it are computed where they are used instead of being hoisted to the
+// kernel entry and kept live (or spilled) across every GEMM
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// v of lane (lane ^ o): ds_bpermute with an index derived from the caller's (opaque) lane
+__device__ __forceinline__ float xor_lane(float v, int lane, int o) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ o) << 2, __float_as_int(v)));
+}
+
 }  // namespace dsr

@@ -896,7 +896,10 @@ struct Jac16Shared {
   float wmax[NWAVE];
 };
 
-template <bool PRIO, bool XP>
+// NB: A ring depth of the split GEMMs (gemm16_sel; 0 = the two-set gemm16_tile).  Lane-derived
+// values are re-derived per layer from an opaque lane id (dsr_mlp_lite.hpp, "Register
+// discipline"); row-selecting conditions are wave-uniform branches + per-lane selects.
+template <bool PRIO, int NB>
 __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
                                                    const ObjDesc* __restrict__ desc,
@@ -911,35 +914,32 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
                                                    float* __restrict__ raw_out,
                                                    float* __restrict__ res_out, MaskArgs MA) {
   __shared__ Jac16Shared sm;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
-  const int T1 = D.Kf[1] / 32;
-  half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
-  if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
-    if (tid < TILE) {
-      float x = 0.f, y = 0.f, z = 0.f, aux = 0.f, rr = 0.f;
-      if (tid < tl.count) {
-        if (tl.term == 0) {
-          const float* p = pts_all + (size_t)(d.pts_off + tl.start + tid) * 3;
-          const float3 xo = xform(st[tl.obj].T, p[0], p[1], p[2]);
-          x = xo.x; y = xo.y; z = xo.z;
-        } else if (tl.term == 1) {
-          const float4 v = kpts[d.cand_off + tl.start + tid];
-          x = v.x; y = v.y; z = v.z; aux = v.w;
-          rr = kres[d.cand_off + tl.start + tid];
-        } else {
-          const float4 v = raw_pts[tl.start + tid];
-          x = v.x; y = v.y; z = v.z;
+    {
+      const int tid = opaque(threadIdx.x);
+      if (tid < TILE) {
+        float x = 0.f, y = 0.f, z = 0.f, aux = 0.f, rr = 0.f;
+        if (tid < tl.count) {
+          if (tl.term == 0) {
+            const float* p = pts_all + (size_t)(d.pts_off + tl.start + tid) * 3;
+            const float3 xo = xform(st[tl.obj].T, p[0], p[1], p[2]);
+            x = xo.x; y = xo.y; z = xo.z;
+          } else if (tl.term == 1) {
+            const float4 v = kpts[d.cand_off + tl.start + tid];
+            x = v.x; y = v.y; z = v.z; aux = v.w;
+            rr = kres[d.cand_off + tl.start + tid];
+          } else {
+            const float4 v = raw_pts[tl.start + tid];
+            x = v.x; y = v.y; z = v.z;
+          }
         }
+        *reinterpret_cast<float4*>(sm.xyz + tid * 4) = make_float4(x, y, z, aux);
+        sm.r[tid] = rr;
       }
-      sm.xyz[tid * 4 + 0] = x; sm.xyz[tid * 4 + 1] = y;
-      sm.xyz[tid * 4 + 2] = z; sm.xyz[tid * 4 + 3] = aux;
-      sm.r[tid] = rr;
     }
     __syncthreads();
     uint64_t mk[8];
@@ -950,11 +950,13 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     // backward chain runs; otherwise the forward recomputes them (loss.py:157)
     bool fast = false;
     if (MA.kslot != nullptr && tl.term == 1) {
+      const int tid = opaque(threadIdx.x);
       int bad = 0;
       if (tid < tl.count) bad = MA.kslot[d.cand_off + tl.start + tid] < 0;
       fast = !__syncthreads_or(bad);
     }
     if (fast) {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
 #pragma unroll
       for (int l = 0; l < 8; ++l) mk[l] = 0;
 #pragma unroll
@@ -971,37 +973,34 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           }
         }
       }
+      const int tid = opaque(threadIdx.x);
       if (tid < TILE)
         sm.y[tid] = (tid < tl.count) ? MA.yv[d.cand_off + MA.kslot[d.cand_off + tl.start + tid]] : 0.f;
-      if constexpr (XP) {                // the prefetched lin1 fragments are not needed: lin7^T
-        const int Tb = D.Kb[7] / 32;
-        load_a0<4>(wfrag(D.Wbh_raw[7], w, Tb), Tb, ah0, al0, lane);
-      }
       __syncthreads();
     } else {
       // ---- lin0 (VALU, fp32) + masks
       {
+        const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
         const float* bias0 = bias0f + tl.obj * HID;
         float m = 0.f;
         mk[0] = 0;
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int n0 = 64 * w + 16 * q + 4 * g;
           const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
           float wx[12];
-  #pragma unroll
+#pragma unroll
           for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
-  #pragma unroll
+#pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
-            const int p = 16 * cb + c;
-            const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
-  #pragma unroll
+            const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+              const float a = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
               const float h = fmaxf(a, 0.f);            // NaN re-imposed after the backward
               if (h > 0.f) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
               v[q][cb][r] = h;
-              m = fmaxf(m, fabsf(h));
+              m = fmaxf(m, h);
             }
           }
         }
@@ -1010,70 +1009,61 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       }
       __syncthreads();
       // ---- forward lin1..lin6 (masks kept)
-  #pragma unroll 1
+#pragma unroll 1
       for (int l = 1; l <= 6; ++l) {
-        const int T = D.Kf[l] / 32;
-        if constexpr (XP) {
-          const int Tn = D.Kf[l + 1] / 32;
-          gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                                 wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
-        } else {
-          gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
-        }
+        const int lane = opaque(threadIdx.x & 63), g = lane >> 4;
+        gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
         const float usc = ldexpf(1.f, -(D.sw[l] + sa));
         const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
         float m = 0.f;
-        mk[l] = 0;
-  #pragma unroll
+        uint64_t bits = 0;
+#pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int n0 = 64 * w + 16 * q + 4 * g;
-          const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
-  #pragma unroll
+          const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
+#pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
-            const int p = 16 * cb + c;
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
-              if (h > 0.f) mk[l] |= 1ull << ((q * 4 + cb) * 4 + r);
-              if (l == 3 && n0 == 444 && r > 0) h = sm.xyz[p * 4 + (r - 1)];
+              const float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+              if (h > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
               v[q][cb][r] = h;
-              m = fmaxf(m, fabsf(h));
+              m = fmaxf(m, h);
             }
           }
         }
+        mk[l] = bits;
+        if (l == 3 && w == 6) xyz_rows(v, sm.xyz, lane, m);     // lin4 input = h3 | xyz
         sa = block_scale(m, sm.wmax, w, lane);
         write_split(v, sa, sm.Hh, sm.Hl, w, lane);
         __syncthreads();
       }
       // ---- lin7 + lin8 dot + tanh
       {
-        const int T = D.Kf[7] / 32;
-        if constexpr (XP) {
-          const int Tn = D.Kb[7] / 32;
-          gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                                 wfrag(D.Wbh_raw[7], w, Tn), Tn);
-        } else {
-          gemm16_tile<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
-        }
+        const int lane = opaque(threadIdx.x & 63);
+        gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane);
         const int un = D.sw[7] + sa;
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 4; ++q)
-  #pragma unroll
+#pragma unroll
           for (int cb = 0; cb < 4; ++cb)
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
         epi_l7(acc, D, sm.red, w, lane, mk[7]);
       }
       __syncthreads();
-      if (tid < TILE) {
-        float s = sm.red[tid];
-        for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
-        sm.y[tid] = tanhf(s + D.b8);
+      {
+        const int tid = opaque(threadIdx.x);
+        if (tid < TILE) {
+          float s = sm.red[tid];
+          for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+          sm.y[tid] = tanhf(s + D.b8);
+        }
       }
       __syncthreads();
     }
     // ---- g7 = (1 - y^2) W8 (.) relu'(a7)
     {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       float m = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1099,39 +1089,42 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     // ---- backward lin7^T .. lin1^T
 #pragma unroll 1
     for (int l = 7; l >= 1; --l) {
-      const int T = D.Kb[l] / 32;
-      if constexpr (XP) {       // next: lin_{l-1}^T, or lin1 of the next tile after lin1^T
-        const _Float16* Wn = (l > 1) ? D.Wbh_raw[l - 1] : D.Wh_raw[1];
-        const int Tn = (l > 1) ? D.Kb[l - 1] / 32 : T1;
-        gemm16_tile_x<PRIO, 4>(wfrag(D.Wbh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                               wfrag(Wn, w, Tn), Tn);
-      } else {
-        gemm16_tile<PRIO, 4>(wfrag(D.Wbh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
-      }
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      gemm16_sel<PRIO, NB>(D.Wbh_raw[l], w, D.Kb[l] / 32, sm.Hh, sm.Hl, acc, lane);
       const float usc = ldexpf(1.f, -(D.swb[l] + sa));
       float m = 0.f;
       const uint64_t mask = mk[l - 1];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n0 = 64 * w + 16 * q + 4 * g;
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const int p = 16 * cb + c;
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int n = n0 + r;
             const float a = accr(acc[q][cb], r) * usc;    // exact (power of two)
-            float gv;
-            if (l == 4 && n >= L3_OUT) {                  // d/d[code, xyz] via the latent skip
-              sm.gin[p * GIN_PITCH + (n - L3_OUT)] = a;
-              gv = 0.f;
-            } else {
-              gv = ((mask >> ((q * 4 + cb) * 4 + r)) & 1ull) ? a : 0.f;
-            }
+            const float gv = ((mask >> ((q * 4 + cb) * 4 + r)) & 1ull) ? a : 0.f;
             v[q][cb][r] = gv;
             m = fmaxf(m, fabsf(gv));
           }
-        }
+      if (l == 4 && w >= 6) {
+        // d/d[code, xyz] via the latent skip: lin3^T's input rows n >= 445 are lin4's code and
+        // xyz columns (wave 7: rows 448..511 all; wave 6: rows 445..447 = q 3, g 3, r 1..3).
+        // Their gradient goes to gin, and they carry no ReLU (mask bit 0 for them: zeroed)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            const int p = 16 * cb + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int n = 64 * w + 16 * q + 4 * g + r;
+              if (w == 7 || (q == 3 && r > 0)) {
+                if (n >= L3_OUT) {
+                  sm.gin[p * GIN_PITCH + (n - L3_OUT)] = accr(acc[q][cb], r) * usc;
+                  v[q][cb][r] = 0.f;
+                }
+              }
+            }
+          }
       }
       sa = block_scale(m, sm.wmax, w, lane);
       write_split(v, sa, sm.Hh, sm.Hl, w, lane);
@@ -1139,6 +1132,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     }
     // ---- lin0^T (80 rows; waves 0..4): d sdf / d input += W0^T g0
     if (w < 5) {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       floatx4 a1[1][4];
       gemm16_tile<PRIO, 1>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
                            sm.Hh, sm.Hl, a1, lane);
@@ -1155,10 +1149,11 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     }
     // torch.relu propagates NaN; the v_max ReLUs above do not, and a NaN can only come in
     // through the point or the code: re-impose it on the outputs of such points
+    const int tid = opaque(threadIdx.x);
     if (tid < TILE) {
-      const float px = sm.xyz[tid * 4 + 0], py = sm.xyz[tid * 4 + 1], pz = sm.xyz[tid * 4 + 2];
+      const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
       const float zprobe = bias0f[tl.obj * HID];
-      if (px != px || py != py || pz != pz || zprobe != zprobe) {
+      if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) {
         sm.y[tid] = __builtin_nanf("");
         for (int e = 0; e < IN; ++e) sm.gin[tid * GIN_PITCH + e] = __builtin_nanf("");
       }

@@ -224,8 +224,8 @@ __device__ __forceinline__ void epi_l7(floatx4 (&acc)[4][4], const DevDecoder& D
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
     float s = part[cb];
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
+    s += xor_lane(s, lane, 16);
+    s += xor_lane(s, lane, 32);
     if (g == 0) red[w * 64 + 16 * cb + c] = s;
   }
 }

@@ -19,6 +19,7 @@
 // 16x16 accumulators, exactly like the fp32 kernel (dsr_mlp.hpp), so the epilogues and
 // the lin8 fusion are shared in structure.
 #pragma once
+#include <utility>
 #include "dsr_dev.hpp"
 #include "dsr_mlp.hpp"
 
@@ -177,6 +178,89 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
   }
 }
 
+// Ring schedule of the split GEMM (cf. gemm_lite in dsr_mlp_lite.hpp): NB k steps of (hi, lo)
+// A fragments in flight through buffer loads (one wave-uniform descriptor, lane offset in one
+// VGPR, (q, k step, piece) offset in an SGPR), the (hi, lo) B pair of the next column block
+// read from LDS as the current block's MFMAs issue, and the three products of an accumulator
+// issued back to back in mfma3_step's order (al.bh, ah.bl, ah.bh) — so the sums are bitwise
+// those of gemm16_tile.  The first step starts from an inline zero C operand.
+template <bool PRIO, int T, int NB>
+__device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Float16* Hh, const _Float16* Hl,
+                                            floatx4 (&acc)[4][4], int lane) {
+  const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
+  const int voff = lane * 16;
+  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const _Float16* Bh = Hh + boff;
+  const _Float16* Bl = Hl + boff;
+  auto lda = [&](int q, int t, int piece) {
+    return __builtin_bit_cast(
+        half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, ((q * T + t) * 2 + piece) * 1024, 0));
+  };
+  half8 ah[NB][4], al[NB][4], bh[2], bl[2];
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ah[j][q] = lda(q, j, 0);
+      al[j][q] = lda(q, j, 1);
+    }
+  bh[0] = *reinterpret_cast<const half8*>(Bh);
+  bl[0] = *reinterpret_cast<const half8*>(Bl);
+  auto step = [&](auto J, auto FIRST, int t) {
+    constexpr int j = decltype(J)::value;
+    if (t + NB - 1 < T) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ah[(j + NB - 1) % NB][q] = lda(q, t + NB - 1, 0);
+        al[(j + NB - 1) % NB][q] = lda(q, t + NB - 1, 1);
+      }
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      // next B pair: block cb+1 of this step, or block 0 of the next one (after the last step
+      // columns 512.. of the 528 pitch / the next point row: in bounds, unused)
+      const int nk = (cb < 3) ? (cb + 1) * 16 * PH + 32 * t : 32 * (t + 1);
+      bh[(cb + 1) & 1] = *reinterpret_cast<const half8*>(Bh + nk);
+      bl[(cb + 1) & 1] = *reinterpret_cast<const half8*>(Bl + nk);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        floatx4 x = decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[j][q], bh[cb & 1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bl[cb & 1], x, 0, 0, 0);
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bh[cb & 1], x, 0, 0, 0);
+      }
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  step(std::integral_constant<int, 0>{}, std::true_type{}, 0);
+  constexpr int TM = 1 + (T - 1) / NB * NB;
+#pragma unroll 1
+  for (int t0 = 1; t0 < TM; t0 += NB) {
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+      (step(std::integral_constant<int, (1 + J) % NB>{}, std::false_type{}, t0 + J), ...);
+    }(std::make_integer_sequence<int, NB>{});
+  }
+  [&]<int... J>(std::integer_sequence<int, J...>) {
+    (step(std::integral_constant<int, (TM + J) % NB>{}, std::false_type{}, TM + J), ...);
+  }(std::make_integer_sequence<int, T - TM>{});
+}
+
+// acc = split product of the wave's 64 rows of packed matrix Wl (K = 32 T, T 16 or 14) and
+// the 64-point image: ring schedule with NB k steps in flight (NB 0: gemm16_tile)
+template <bool PRIO, int NB>
+__device__ __forceinline__ void gemm16_sel(const _Float16* Wl, int w, int T, const _Float16* Hh,
+                                           const _Float16* Hl, floatx4 (&acc)[4][4], int lane) {
+  if constexpr (NB == 0) {
+    gemm16_tile<PRIO, 4>(wfrag(Wl, w, T), T, Hh, Hl, acc, lane);
+  } else {
+    if (T != 14) gemm16_ring<PRIO, 16, NB>(Wl, w, Hh, Hl, acc, lane);
+    else gemm16_ring<PRIO, 14, NB>(Wl, w, Hh, Hl, acc, lane);
+  }
+}
+
 // power-of-two scale exponent s such that m * 2^s < 2^14 (m >= 0); 0 for m == 0 / non-finite
 __device__ __forceinline__ int act_scale_exp(float m) {
   if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
@@ -185,29 +269,16 @@ __device__ __forceinline__ int act_scale_exp(float m) {
   return 14 - e;
 }
 
-// x, re-materialised at this point: the compiler may not assume it equals an earlier x, so
-// values derived from it are computed where they are used instead of being hoisted to the
-// kernel entry and kept live (or spilled) across every GEMM
-__device__ __forceinline__ int opaque(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
-// v of lane (lane ^ o): ds_bpermute with an index derived from the caller's (opaque) lane
-__device__ __forceinline__ float xor_lane(float v, int lane, int o) {
-  return __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ o) << 2, __float_as_int(v)));
-}
-
-__device__ __forceinline__ float wave_max(float v) {
+__device__ __forceinline__ float wave_max(float v, int lane) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, xor_lane(v, lane, o));
   return v;
 }
 
 // Workgroup max of |v| -> power-of-two scale exponent.  Contains the barrier that
 // separates the previous GEMM's reads of the image from the writes of the next one.
 __device__ __forceinline__ int block_scale(float m, float* wmax, int w, int lane) {
-  m = wave_max(m);
+  m = wave_max(m, lane);
   if (lane == 0) wmax[w] = m;
   __syncthreads();
   float mm = wmax[0];
@@ -270,6 +341,23 @@ __device__ __forceinline__ uint64_t relu_bits(const float (&v)[4][4][4]) {
   return mk;
 }
 
+// lin4's input is h3 | xyz: lin3's padded output rows 445..447 (wave 6, q 3, g 3, r 1..3)
+// carry the point's x, y, z.  Called under a wave-uniform branch (w == 6); the row choice
+// is a per-lane select, not a per-element divergent branch.  m takes their magnitudes.
+template <int NCB>
+__device__ __forceinline__ void xyz_rows(float (&v)[4][NCB][4], const float* xyz, int lane, float& m) {
+  const int g = lane >> 4, c = lane & 15;
+  const bool on = g == 3;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const float4 p = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+    v[3][cb][1] = on ? p.x : v[3][cb][1];
+    v[3][cb][2] = on ? p.y : v[3][cb][2];
+    v[3][cb][3] = on ? p.z : v[3][cb][3];
+    m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+  }
+}
+
 __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
                                      Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk) {
   const int g = lane >> 4, c = lane & 15;
@@ -283,20 +371,19 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
     const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-      const int p = 16 * cb + c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // acc*2^-unscale is exact, so the fma rounds exactly like (acc*2^-un) + b; ReLU as
         // v_max (NaN inputs are re-imposed on the output, see nan_in below)
-        float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+        const float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
         if (x > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
-        if (is_l3 && n0 == 444 && r > 0) x = sm.xyz[p * 4 + (r - 1)];
         v[q][cb][r] = x;
-        m = fmaxf(m, fabsf(x));           // (xyz rows of lin3 may be negative)
+        m = fmaxf(m, x);
       }
     }
   }
-  m = wave_max(m);
+  if (is_l3 && w == 6) xyz_rows(v, sm.xyz, lane, m);
+  m = wave_max(m, lane);
   if (lane == 0) sm.wmax[w] = m;
   __syncthreads();                       // all waves done reading H; maxima published
   float mm = sm.wmax[0];
@@ -308,8 +395,8 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
   return s;
 }
 
-// X: bit0 cross-layer A prefetch; bits 1-2 = timing experiments only (results invalid):
-// 2 = epilogue reduced to one fp16 store, 4 = no epilogue (GEMMs + barriers only).
+// X: bit9 (512) exact re-decode of lite band samples — keep their ReLU masks + sdf
+// (MaskArgs); bits 10-11 = NB - 1 of the ring GEMM (gemm16_sel; 0 = the two-set gemm16_tile).
 template <bool PRIO, int X>
 __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
@@ -320,29 +407,25 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
                                                    float* __restrict__ dense, unsigned* __restrict__,
                                                    ErtArgs E, MaskArgs MA) {
   __shared__ Fwd16Shared sm;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
-  constexpr bool XP = (X & 1) != 0;
-  constexpr int EXPM = X & 6;
-  constexpr int EX = (X >> 3) & 3;
-  constexpr bool MSK = (X & 512) != 0;     // exact re-decode: keep masks + sdf (MaskArgs)
-  const int T1 = D.Kf[1] / 32;
-  half8 ah0[4], al0[4];                 // next GEMM's first A fragments (XP)
-  if constexpr (XP) load_a0<4>(wfrag(D.Wh_raw[1], w, T1), T1, ah0, al0, lane);
+  constexpr bool MSK = (X & 512) != 0;
+  constexpr int NB = ((X >> 10) & 3) == 0 ? 0 : 1 + ((X >> 10) & 3);
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
-    if (tid < TILE) {
-      const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
-      sm.xyz[tid * 4 + 0] = v.x; sm.xyz[tid * 4 + 1] = v.y;
-      sm.xyz[tid * 4 + 2] = v.z; sm.xyz[tid * 4 + 3] = v.w;
+    {
+      const int tid = opaque(threadIdx.x);
+      if (tid < TILE) {
+        const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(sm.xyz + tid * 4) = v;
+      }
     }
     __syncthreads();
     // ---- lin0 on VALU (fp32), then split
     int sa;
     {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       const float* bias0 = bias0f + tl.obj * HID;
       float v[4][4][4];
       float m = 0.f;
@@ -355,62 +438,33 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          const int p = 16 * cb + c;
-          const float x = sm.xyz[p * 4 + 0], y = sm.xyz[p * 4 + 1], z = sm.xyz[p * 4 + 2];
+          const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float a = fetch4(bb, r) + ((wx[3 * r] * x + wx[3 * r + 1] * y) + wx[3 * r + 2] * z);
+            const float a = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
             v[q][cb][r] = fmaxf(a, 0.f);
             m = fmaxf(m, v[q][cb][r]);
           }
         }
       }
-      m = wave_max(m);
-      if (lane == 0) sm.wmax[w] = m;
-      __syncthreads();
-      float mm = sm.wmax[0];
-#pragma unroll
-      for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
-      sa = act_scale_exp(mm);
+      sa = block_scale(m, sm.wmax, w, lane);
       write_split(v, sa, sm.Hh, sm.Hl, w, lane);
       if constexpr (MSK) store_mask16(relu_bits(v), MA.msk, d.cand_off + tl.start, tl.count, 0, w, lane);
     }
     __syncthreads();
     floatx4 acc[4][4];
+#pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
-      const int T = D.Kf[l] / 32;
-      if constexpr (XP) {
-        const int Tn = D.Kf[l + 1] / 32;
-        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                               wfrag(D.Wh_raw[l + 1], w, Tn), Tn);
-      } else {
-        gemm16_tile<PRIO, 4, EX>(wfrag(D.Wh_raw[l], w, T), T, sm.Hh, sm.Hl, acc, lane);
-      }
-      if constexpr (EXPM == 0) {
-        uint64_t mk;
-        sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
-        if constexpr (MSK) store_mask16(mk, MA.msk, d.cand_off + tl.start, tl.count, l, w, lane);
-      } else if constexpr (EXPM == 2) {
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            half4 hh;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) hh[r] = (_Float16)accr(acc[q][cb], r);
-            *reinterpret_cast<half4*>(sm.Hh + (16 * cb + c) * PH + 64 * w + 16 * q + 4 * g) = hh;
-          }
-      }
+      const int lane = opaque(threadIdx.x & 63);
+      gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
+      uint64_t mk;
+      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
+      if constexpr (MSK) store_mask16(mk, MA.msk, d.cand_off + tl.start, tl.count, l, w, lane);
       __syncthreads();
     }
     {
-      const int T = D.Kf[7] / 32;
-      if constexpr (XP)      // prefetch lin1 of the next tile (same weights every tile)
-        gemm16_tile_x<PRIO, 4>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane, ah0, al0,
-                               wfrag(D.Wh_raw[1], w, T1), T1);
-      else
-        gemm16_tile<PRIO, 4, EX>(wfrag(D.Wh_raw[7], w, T), T, sm.Hh, sm.Hl, acc, lane);
+      const int lane = opaque(threadIdx.x & 63);
+      gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane);
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -423,23 +477,26 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       if constexpr (MSK) store_mask16(mask, MA.msk, d.cand_off + tl.start, tl.count, 7, w, lane);
     }
     __syncthreads();
-    if (tid < tl.count) {
-      float s = sm.red[tid];
-      for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
-      float y = tanhf(s + D.b8);
-      // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
-      // enter through the point or the code, so re-impose it here
-      const float px = sm.xyz[tid * 4 + 0], py = sm.xyz[tid * 4 + 1], pz = sm.xyz[tid * 4 + 2];
-      const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
-      if (px != px || py != py || pz != pz || zprobe != zprobe) y = __builtin_nanf("");
-      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
-      if (E.st) {                        // re-decode of a lite band sample: track the lite error
-        const float e = fabsf(y - dense[d.cand_off + idx]);
-        if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+    {
+      const int tid = opaque(threadIdx.x);
+      if (tid < tl.count) {
+        float s = sm.red[tid];
+        for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
+        float y = tanhf(s + D.b8);
+        // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
+        // enter through the point or the code, so re-impose it here
+        const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
+        const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
+        if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) y = __builtin_nanf("");
+        const int idx = __float_as_int(p.w);
+        if (E.st) {                        // re-decode of a lite band sample: track the lite error
+          const float e = fabsf(y - dense[d.cand_off + idx]);
+          if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+        }
+        dense[d.cand_off + idx] = y;
+        if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
+        if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
       }
-      dense[d.cand_off + idx] = y;
-      if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
-      if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
     }
     __syncthreads();
   }

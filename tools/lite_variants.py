@@ -1,6 +1,7 @@
-"""A/B the lite-pass kernel variants (DSR_LITE_VARIANT) in ONE process, interleaved.
+"""A/B kernel variants (an env switch: DSR_LITE_VARIANT, DSR_SPLIT_RING, ...) in ONE process,
+interleaved.
 
-Usage (GPU box): python tools/lite_variants.py 0 16 32 48 [--diag 1 2] [--rounds 5] [--iters 1]
+Usage (GPU box): python tools/lite_variants.py 16 24 [--var DSR_LITE_VARIANT] [--diag 18] [--rounds 5] [--iters 1]
 Each run is a batch of `--iters` GN iterations over 64 KITTI-like objects.  Prints the median
 lite-kernel ms per launch and TFLOP/s (one fp16 product per MAC), and checks that every
 non-diagnostic variant returns results bitwise equal to the first one (the variants only change
@@ -28,6 +29,7 @@ ap.add_argument("--diag", nargs="*", type=int, default=[])
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--objects", type=int, default=64)
 ap.add_argument("--iters", type=int, default=1)
+ap.add_argument("--var", default="DSR_LITE_VARIANT")
 a = ap.parse_args()
 dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS)
 cfg = dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=a.iters))
@@ -40,13 +42,14 @@ ref = None
 bad = []
 for r in range(a.rounds):
     for v in allv:
-        os.environ["DSR_LITE_VARIANT"] = str(v)
+        os.environ[a.var] = str(v)
         ctx.check(lib.dsr_batch_run(batch), "run")
         ctx.check(lib.dsr_batch_download(batch, outs), "dl")
         st = L.Stats()
         ctx.check(lib.dsr_batch_stats(batch, C.byref(st)), "stats")
         res[v].append((st.fwd_ms / max(1, st.fwd_launches), st.fwd_ms, st.total_ms,
-                       2 * bench.FWD_MAC * st.fwd_points / (st.fwd_ms * 1e-3) / 1e12, st.fwd_points))
+                       2 * bench.FWD_MAC * st.fwd_points / (st.fwd_ms * 1e-3) / 1e12, st.fwd_points,
+                       st.refine_ms, st.jac_ms))
         if v in a.variants:
             sig = np.array([list(outs[i].t_cam_obj) + list(outs[i].code) + [outs[i].loss]
                             for i in range(a.objects)], np.float32)
@@ -57,7 +60,7 @@ for r in range(a.rounds):
 for v in allv:
     x = np.median(np.array(res[v]), axis=0)
     tag = "diag" if v in a.diag else ("DIFFERS" if v in bad else "bitwise-equal")
-    print(f"lite V{v:3d}: {x[0]:6.3f} ms/launch  {x[1]:7.2f} ms/run  total {x[2]:7.2f} ms  "
-          f"{x[3]:7.1f} TF  pts {int(x[4])}  [{tag}]", flush=True)
+    print(f"{a.var}={v}: lite {x[0]:6.3f} ms/launch {x[1]:7.2f} ms/run {x[3]:7.1f} TF | exact band "
+          f"{x[5]:6.2f} ms | jac {x[6]:6.2f} ms | total {x[2]:7.2f} ms | pts {int(x[4])}  [{tag}]", flush=True)
 if bad:
     sys.exit(1)
