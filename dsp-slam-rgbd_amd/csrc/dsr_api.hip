@@ -86,11 +86,12 @@ static JacKernel jac_kernel() {
   return k_mlp_jac;
 }
 // Lite-pass variant (DSR_LITE_VARIANT, dsr_mlp_lite.hpp: lite_gemm): 16/32/48 = A ring of
-// 2/3/4 k steps, +8 static activation scale; 18 is a timing experiment (no A streaming)
+// 2/3/4 k steps, +8 static activation scale, +64 ring carried across layers (default 88);
+// 18 is a timing experiment (no A streaming)
 using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                             const float*, float*, ErtArgs);
 #ifndef DSR_DEFAULT_LITE_VARIANT
-#define DSR_DEFAULT_LITE_VARIANT 24
+#define DSR_DEFAULT_LITE_VARIANT 88
 #endif
 static LiteKernel lite_kernel() {
   const char* e = getenv("DSR_LITE_VARIANT");
@@ -101,8 +102,9 @@ static LiteKernel lite_kernel() {
     case 40: return k_mlp_fwd_lite<true, 40>;
     case 48: return k_mlp_fwd_lite<true, 48>;
     case 56: return k_mlp_fwd_lite<true, 56>;
+    case 24: return k_mlp_fwd_lite<true, 24>;
   }
-  return k_mlp_fwd_lite<true, 24>;
+  return k_mlp_fwd_lite<true, 88>;
 }
 static int fwd_variant() {
   const char* e = getenv("DSR_FWD_VARIANT");

@@ -45,6 +45,10 @@ struct LiteShared {
   float red[NWAVE * LTILE];
   float wmax[NWAVE];
   int ovf;
+  // LV bit6 (cross-layer prefetch): the epilogue reads its bias from LDS, so no vector global
+  // load waits behind the next layer's in-flight weight fragments (vmcnt counts in order)
+  float bias[8][HID];          // lin0..lin7 (0 and 4: this tile's object, folded code)
+  float w8[HID];
 };
 
 // acc[4][8] = hi(A rows of this wave) . hi(H) over K = 32*T.
@@ -107,8 +111,70 @@ __device__ __forceinline__ void gemm_lite(const _Float16* Wl, int w, const _Floa
   }(std::make_integer_sequence<int, T - TM>{});
 }
 
+// gemm_lite with the ring carried across GEMMs (NB = 2; every T is even, so step t of every
+// matrix uses slot t % 2): on entry a[0] holds step 0 of this matrix, and its last step loads
+// step 0 of the NEXT matrix (Wn, Tn k steps) into a[0], so that load's L2 latency hides behind
+// this layer's last MFMAs and the epilogue instead of stalling the next layer's first MFMA.
+template <bool PRIO, int T, int LV>
+__device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* Wn, int Tn, int w,
+                                            const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4],
+                                            int lane) {
+  const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
+  const int voff = lane * 16;
+  const _Float16* B = H + (lane & 15) * PH + 8 * (lane >> 4);
+  auto lda = [&](int q, int t) {
+    return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (q * T + t) * 2048, 0));
+  };
+  auto ldb = [&](int cb, int k32) { return *reinterpret_cast<const half8*>(B + cb * 16 * PH + k32); };
+  half8 b[4];
+#pragma unroll
+  for (int cb = 0; cb < 3; ++cb) b[cb] = ldb(cb, 0);
+  auto step = [&](auto J, auto FIRST, int t) {
+    constexpr int j = decltype(J)::value;
+    if (t + 1 < T) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[j ^ 1][q] = lda(q, t + 1);
+    }
+    const int pc = 32 * t, pn = 32 * (t + 1);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      b[(cb + 3) & 3] = (cb + 3 < 8) ? ldb(cb + 3, pc) : ldb(cb - 5, pn);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+            a[j][q], b[cb & 3], decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb], 0, 0, 0);
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  step(std::integral_constant<int, 0>{}, std::true_type{}, 0);
+#pragma unroll 1
+  for (int t0 = 1; t0 < T - 1; t0 += 2) {
+    step(std::integral_constant<int, 1>{}, std::false_type{}, t0);
+    step(std::integral_constant<int, 0>{}, std::false_type{}, t0 + 1);
+  }
+  {   // the next matrix's first step, into the slot step T-2 released
+    const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<_Float16*>(Wn + (size_t)(4 * w) * Tn * 2 * 64 * 8), 0, 4 * Tn * 2 * 1024, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      a[0][q] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, q * Tn * 2048, 0));
+  }
+  step(std::integral_constant<int, 1>{}, std::false_type{}, T - 1);
+}
+
+template <bool PRIO, int LV>
+__device__ __forceinline__ void lite_gemm_x(const _Float16* Wl, int T, const _Float16* Wn, int Tn, int w,
+                                            const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4], int lane) {
+  if (T != 14) gemm_lite_x<PRIO, 16, LV>(Wl, Wn, Tn, w, H, acc, a, lane);
+  else gemm_lite_x<PRIO, 14, LV>(Wl, Wn, Tn, w, H, acc, a, lane);
+}
+
 // LV (DSR_LITE_VARIANT): bits 4-5 = NB - 1 (ring depth; 0 is read as NB 2), bit3 static
-// activation scale (lite_scale), bit1 timing experiment (no A streaming).
+// activation scale (lite_scale), bit6 the NB-2 ring carried across layers and tiles
+// (gemm_lite_x; biases read from LDS), bit1 timing experiment (no A streaming).
 template <bool PRIO, int LV>
 __device__ __forceinline__ void lite_gemm(const _Float16* Wl, int w, int T, const _Float16* H,
                                           floatx4 (&acc)[4][8], int lane) {
@@ -169,6 +235,24 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
   __shared__ LiteShared sm;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
+  constexpr bool XL = (LV & 64) != 0;     // ring carried across layers, biases in LDS
+  half8 ring[2][4];
+  if constexpr (XL) {
+    const int tid = opaque(threadIdx.x);
+    for (int e = tid; e < 7 * HID; e += 512) {
+      const int l = e / HID, n = e - l * HID;        // lin1..3, lin5..7, W8
+      if (l < 6) sm.bias[l < 3 ? l + 1 : l + 2][n] = D.bias[l < 3 ? l + 1 : l + 2][n];
+      else sm.w8[n] = D.W8[n];
+    }
+    const int lane = tid & 63;
+    const _Float16* A1 = D.Wh_raw[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * 2 * 64 * 8;
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<_Float16*>(A1), 0, 4 * (D.Kf[1] / 32) * 2 * 1024, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ring[0][q] = __builtin_bit_cast(
+          half8, __builtin_amdgcn_raw_buffer_load_b128(r1, lane * 16, q * (D.Kf[1] / 32) * 2048, 0));
+  }
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
@@ -179,6 +263,13 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
         *reinterpret_cast<float4*>(sm.xyz + tid * 4) = v;
       }
       if (tid == 0) sm.ovf = 0;
+      if constexpr (XL) {                  // this object's folded lin0 / lin4 biases
+        if (tid < 256) {
+          const float* src = (tid < 128 ? bias0f : bias4f) + tl.obj * HID + 4 * (tid & 127);
+          *reinterpret_cast<float4*>(&sm.bias[tid < 128 ? 0 : 4][4 * (tid & 127)]) =
+              *reinterpret_cast<const float4*>(src);
+        }
+      }
     }
     __syncthreads();
     floatx4 acc[4][8];
@@ -186,7 +277,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
     // ---- lin0 (3 inputs, fp32 VALU) into the accumulator layout
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
-      const float* bias0 = bias0f + tl.obj * HID;
+      const float* bias0 = XL ? sm.bias[0] : bias0f + tl.obj * HID;
       float m = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -215,9 +306,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
 #pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
-      lite_gemm<PRIO, LV>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.H, acc, lane);
+      if constexpr (XL)
+        lite_gemm_x<PRIO, LV>(D.Wh_raw[l], D.Kf[l] / 32, D.Wh_raw[l + 1], D.Kf[l + 1] / 32, w, sm.H, acc, ring, lane);
+      else
+        lite_gemm<PRIO, LV>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.H, acc, lane);
       const float usc = ldexpf(1.f, -(D.sw[l] + sa));
-      const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
+      const float* bias = XL ? sm.bias[l] : (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
       float m = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -250,16 +344,21 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
     // ---- lin7 + relu, lin8 dot product, tanh
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
-      lite_gemm<PRIO, LV>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.H, acc, lane);
+      if constexpr (XL)     // (the next tile's lin1 fragments: same weights every tile)
+        lite_gemm_x<PRIO, LV>(D.Wh_raw[7], D.Kf[7] / 32, D.Wh_raw[1], D.Kf[1] / 32, w, sm.H, acc, ring, lane);
+      else
+        lite_gemm<PRIO, LV>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.H, acc, lane);
       const float usc = ldexpf(1.f, -(D.sw[7] + sa));
+      const float* b7 = XL ? sm.bias[7] : D.bias[7];
+      const float* w8p = XL ? sm.w8 : D.W8;
       float part[8];
 #pragma unroll
       for (int cb = 0; cb < 8; ++cb) part[cb] = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = 64 * w + 16 * q + 4 * g;
-        const float4 bb = *reinterpret_cast<const float4*>(D.bias[7] + n0);
-        const float4 w8 = *reinterpret_cast<const float4*>(D.W8 + n0);
+        const float4 bb = *reinterpret_cast<const float4*>(b7 + n0);
+        const float4 w8 = *reinterpret_cast<const float4*>(w8p + n0);
 #pragma unroll
         for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
