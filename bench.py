@@ -111,7 +111,7 @@ def pmc_traffic(kernel="k_mlp_fwd16"):
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json")), key=os.path.getmtime):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json"))):   # tag order r1 < r1b < ...
         try:
             d = json.load(open(f))
         except Exception:

@@ -103,8 +103,21 @@ static LiteKernel lite_kernel() {
     case 48: return k_mlp_fwd_lite<true, 48>;
     case 56: return k_mlp_fwd_lite<true, 56>;
     case 24: return k_mlp_fwd_lite<true, 24>;
+    case 216: return k_mlp_fwd_lite_st<true, 88>;     // 88 + staggered groups (bit7)
   }
   return k_mlp_fwd_lite<true, 88>;
+}
+// DSR_REFINE_ALL=1: the exact pass re-decodes every band sample, also those behind a ray's
+// first certainly-full sample (k_refine_compact)
+static bool refine_all() {
+  const char* e = getenv("DSR_REFINE_ALL");
+  return e && atoi(e) != 0;
+}
+// DSR_LITE_LAG (staggered lite kernel): the k step group A reaches before group B starts a GEMM
+static int lite_lag() {
+  const char* e = getenv("DSR_LITE_LAG");
+  const int v = e ? atoi(e) : 4;
+  return v < 0 ? 0 : (v > 7 ? 7 : v);
 }
 static int fwd_variant() {
   const char* e = getenv("DSR_FWD_VARIANT");
@@ -767,7 +780,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       float* b4 = b->bias4f + (size_t)o0 * HID;
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
-      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine};
+      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
@@ -787,7 +800,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
         if (b->ma.slotmap)
           DSR_CHECK(ctx, hipMemsetAsync(b->ma.slotmap + gr.c0, 0xff, sizeof(int) * (size_t)(gr.c1 - gr.c0), s));
         hipLaunchKernelGGL(k_refine_compact, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->cand, b->refine, b->ma.slotmap);
+                           b->cand, b->refine, b->ma.slotmap, refine_all() ? nullptr : b->dense, -P.cut_off);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};

@@ -97,6 +97,7 @@ struct ErtArgs {
   float nth;             // -cut_off
   ObjState* st;          // lite pass: per-object margin; exact re-decode: per-object error
   unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
+  int lag;               // staggered lite pass: k step at which group B may start a GEMM
 };
 
 // ReLU masks + SDF of the samples the exact pass re-decodes after the lite pass, so the

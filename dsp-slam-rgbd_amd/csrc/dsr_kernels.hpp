@@ -362,12 +362,21 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
 // k_refine_compact: the samples the lite pass left in the +-(th + margin) band
 // (dsr_mlp_lite.hpp), (ray, depth)-ordered into cand for the exact split-fp16 pass;
 // clears the flags it consumes.  One thread per ray, one workgroup per object.
+// A ray's scan stops at its first certainly-full sample (an unflagged lite value
+// <= -th - margin, the criterion that set `dead`): its exact sdf is <= -th, so the
+// transmittance is exactly 0 behind it and every later sample enters d_u, de_do and K
+// (loss.py:111-135) multiplied by that zero (the early-termination argument, DESIGN
+// §3.3) — band samples there need no exact value.  Every sample in front of it was
+// decoded by this iteration's passes (in-ball rank = depth order), and out-of-ball
+// samples hold NaN, so the scan reads only this iteration's values.  `dense` == nullptr
+// refines every flagged sample (DSR_REFINE_ALL=1).
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, const ObjDesc* __restrict__ desc,
                                                                    ObjState* st, const float* __restrict__ rays_all,
                                                                    int M, float4* __restrict__ cand,
                                                                    unsigned char* __restrict__ refine,
-                                                                   int* __restrict__ slotmap) {
+                                                                   int* __restrict__ slotmap,
+                                                                   const float* __restrict__ dense, float nth) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -382,9 +391,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
     const int ray = r0 + tid;
     unsigned char* f = refine + d.cand_off + (size_t)ray * M;
     uint64_t bits = 0;
-    if (ray < d.n_rays)
-      for (int j = 0; j < M; ++j)
+    if (ray < d.n_rays) {
+      const float full = nth - S.lite_margin;
+      const float* y = dense ? dense + d.cand_off + (size_t)ray * M : nullptr;
+      int j = 0;
+      for (; j < M; ++j) {
         if (f[j]) { bits |= 1ull << j; f[j] = 0; }
+        else if (y && y[j] <= full) { ++j; break; }
+      }
+      for (; j < M; ++j) f[j] = 0;          // behind the terminating sample: not refined
+    }
     const int cnt = __popcll(bits);
     const int inc = wave_incl_scan(cnt, lane);
     if (lane == 63) wsum[wv] = inc;

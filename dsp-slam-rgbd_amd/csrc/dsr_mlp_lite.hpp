@@ -115,10 +115,16 @@ __device__ __forceinline__ void gemm_lite(const _Float16* Wl, int w, const _Floa
 // matrix uses slot t % 2): on entry a[0] holds step 0 of this matrix, and its last step loads
 // step 0 of the NEXT matrix (Wn, Tn k steps) into a[0], so that load's L2 latency hides behind
 // this layer's last MFMAs and the epilogue instead of stalling the next layer's first MFMA.
-template <bool PRIO, int T, int LV>
+// `hook(t)` runs at the start of k step t, before that step's loads (the staggered kernel's
+// event waits and signals, k_mlp_fwd_lite_st); the default does nothing.
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <bool PRIO, int T, int LV, class Hook = NoHook>
 __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* Wn, int Tn, int w,
                                             const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4],
-                                            int lane) {
+                                            int lane, Hook hook = Hook{}) {
   const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
@@ -133,6 +139,7 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
   for (int cb = 0; cb < 3; ++cb) b[cb] = ldb(cb, 0);
   auto step = [&](auto J, auto FIRST, int t) {
     constexpr int j = decltype(J)::value;
+    hook(t);
     if (t + 1 < T) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) a[j ^ 1][q] = lda(q, t + 1);
@@ -165,11 +172,12 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
   step(std::integral_constant<int, 1>{}, std::false_type{}, T - 1);
 }
 
-template <bool PRIO, int LV>
+template <bool PRIO, int LV, class Hook = NoHook>
 __device__ __forceinline__ void lite_gemm_x(const _Float16* Wl, int T, const _Float16* Wn, int Tn, int w,
-                                            const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4], int lane) {
-  if (T != 14) gemm_lite_x<PRIO, 16, LV>(Wl, Wn, Tn, w, H, acc, a, lane);
-  else gemm_lite_x<PRIO, 14, LV>(Wl, Wn, Tn, w, H, acc, a, lane);
+                                            const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4], int lane,
+                                            Hook hook = Hook{}) {
+  if (T != 14) gemm_lite_x<PRIO, 16, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook);
+  else gemm_lite_x<PRIO, 14, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook);
 }
 
 // LV (DSR_LITE_VARIANT): bits 4-5 = NB - 1 (ring depth; 0 is read as NB 2), bit3 static
@@ -394,6 +402,250 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
       }
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Staggered groups (DSR_LITE_VARIANT bit7, on top of 88's cross-layer ring, static scale and
+// LDS biases).  With one barrier per layer all 8 waves run their epilogues together and the
+// MFMA pipes idle meanwhile.  Here waves 0-3 (group A: rows 0..255 = the next GEMM's k steps
+// 0..7) and waves 4-7 (group B: rows 256..511 = k steps 8..15) synchronise through event
+// counters in LDS instead, so B can trail A and each SIMD's two waves (w, w+4) overlap one
+// wave's epilogue with the other's MFMAs.  Same MFMAs in the same k order as variant 88, so
+// the lite values are bitwise those of 88.  Events (monotonic; a wave adds 1 per event):
+//   cH[g]  group g wrote its rows of the current image (or, at lin7, its part of `red`)
+//   cRlo   a wave finished reading k steps 0..7 of a GEMM's input (signalled at step 8)
+//   cRhi   a wave finished the GEMM (all its reads)
+//   cP     an A wave reached k step `lag` of a GEMM (B starts a GEMM only then: the stagger)
+//   cT[g]  group g's tile inputs (its xyz copy, its rows of the object's lin0/lin4 biases)
+//   cE     a B wave finished a tile (B's xyz copy is read until the last B wave is done)
+// Dependencies per GEMM: k steps 0..7 need cH[A], 8..15 cH[B] of the previous image; A may
+// overwrite its rows once every wave passed step 8 (cRlo), B once every wave finished (cRhi).
+// Every wait is bounded: a wave that waits ~2^16 polls marks the block broken, skips all
+// further waits and sends every sample it classifies to the exact pass (results stay exact).
+struct LiteStShared {
+  _Float16 H[LTILE * PH];
+  float xyz[2][LTILE * 4];     // per group
+  float red[NWAVE * LTILE];
+  float bias[8][HID];
+  float w8[HID];
+  int ovf[2];                  // per tile parity: (tile iteration + 1) if a value reached 2^15
+  int cH[2], cRlo, cRhi, cP, cT[2], cE, broken, pad[7];
+};
+
+__device__ __forceinline__ void st_signal(int* c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (__lane_id() == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void st_wait(int* c, int target, int* broken) {
+  int n = 0;
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+         target) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+      break;
+    if (++n > (1 << 16)) {
+      __hip_atomic_store(broken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+
+template <bool PRIO, int LV>
+__global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Tile* __restrict__ tiles,
+                                                         const int* __restrict__ n_tiles,
+                                                         const ObjDesc* __restrict__ desc,
+                                                         const float4* __restrict__ cand,
+                                                         const float* __restrict__ bias0f,
+                                                         const float* __restrict__ bias4f,
+                                                         float* __restrict__ dense, ErtArgs E) {
+  __shared__ LiteStShared sm;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = w >> 2;
+  const int nt = *n_tiles;
+  const int lag = E.lag;
+  half8 ring[2][4];
+  {
+    const int tid = opaque(threadIdx.x);
+    for (int e = tid; e < 7 * HID; e += 512) {
+      const int l = e / HID, n = e - l * HID;        // lin1..3, lin5..7, W8
+      if (l < 6) sm.bias[l < 3 ? l + 1 : l + 2][n] = D.bias[l < 3 ? l + 1 : l + 2][n];
+      else sm.w8[n] = D.W8[n];
+    }
+    if (tid < 18) (&sm.ovf[0])[tid] = 0;
+    const int lane = tid & 63;
+    const _Float16* A1 = D.Wh_raw[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * 2 * 64 * 8;
+    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<_Float16*>(A1), 0, 4 * (D.Kf[1] / 32) * 2 * 1024, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ring[0][q] = __builtin_bit_cast(
+          half8, __builtin_amdgcn_raw_buffer_load_b128(r1, lane * 16, q * (D.Kf[1] / 32) * 2048, 0));
+  }
+  __syncthreads();                       // the only block-wide barrier
+  int it = 0;
+  for (int ti = blockIdx.x; ti < nt; ti += gridDim.x, ++it) {
+    const int p = it & 1;
+    const Tile tl = tiles[ti];
+    const ObjDesc d = desc[tl.obj];
+    float* xyz = sm.xyz[grp];
+    // ---- tile inputs, per group
+    {
+      const int lane = opaque(threadIdx.x & 63);
+      if (grp == 1) st_wait(&sm.cE, 4 * it, &sm.broken);
+      const int gt = opaque(threadIdx.x) & 255;
+      if (gt < LTILE) {
+        const float4 v = (gt < tl.count) ? cand[d.cand_off + tl.start + gt] : make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(xyz + gt * 4) = v;
+      } else {
+        const int e = gt - LTILE, which = e >> 6, n = 256 * grp + 4 * (e & 63);
+        const float* src = (which == 0 ? bias0f : bias4f) + tl.obj * HID + n;
+        *reinterpret_cast<float4*>(&sm.bias[which == 0 ? 0 : 4][n]) = *reinterpret_cast<const float4*>(src);
+      }
+      st_signal(&sm.cT[grp]);
+      st_wait(&sm.cT[grp], 4 * (it + 1), &sm.broken);
+    }
+    floatx4 acc[4][8];
+    // ---- lin0 (3 inputs, fp32 VALU) into the accumulator layout
+    {
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      const float* bias0 = sm.bias[0];
+      float m = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4*>(bias0 + n0);
+        float wx[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) wx[i] = D.W0x[n0 * 3 + i];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+          const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a = fetch4(bb, r) + ((wx[3 * r] * pt.x + wx[3 * r + 1] * pt.y) + wx[3 * r + 2] * pt.z);
+            const float h = fmaxf(a, 0.f);
+            acc[q][cb][r] = h;
+            m = fmaxf(m, h);
+          }
+        }
+      }
+      if (!(m < 32768.f)) sm.ovf[p] = it + 1;
+      st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * 7 * it, &sm.broken);   // readers of lin7's input
+      lite_write(acc, 0, sm.H, w, lane);
+      st_signal(&sm.cH[grp]);
+    }
+    // ---- lin1..lin7 (lin7: + relu, lin8 dot product -> red)
+    auto gemm = [&](int l) {
+      const int ng = 7 * it + l;         // GEMMs so far, this one included
+      const int hs = 4 * (8 * it + l);   // cH count once the input image is complete
+      st_wait(&sm.cH[0], hs, &sm.broken);
+      if (grp == 1) {
+        st_wait(&sm.cH[1], hs, &sm.broken);
+        if (lag > 0) st_wait(&sm.cP, 4 * ng, &sm.broken);
+      }
+      auto hook = [&](int t) {
+        if (t == 7 && grp == 0) st_wait(&sm.cH[1], hs, &sm.broken);
+        if (t == 8) st_signal(&sm.cRlo);
+        if (t == lag && grp == 0) st_signal(&sm.cP);
+      };
+      const int ln = l < 7 ? l + 1 : 1;  // (after lin7: the next tile's lin1 fragments)
+      lite_gemm_x<PRIO, LV>(D.Wh_raw[l], D.Kf[l] / 32, D.Wh_raw[ln], D.Kf[ln] / 32, w, sm.H, acc, ring,
+                            opaque(threadIdx.x & 63), hook);
+      st_signal(&sm.cRhi);
+    };
+#pragma unroll 1
+    for (int l = 1; l <= 6; ++l) {
+      gemm(l);
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      const float usc = ldexpf(1.f, -D.sw[l]);
+      const float* bias = sm.bias[l];
+      float m = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+            acc[q][cb][r] = x;
+            m = fmaxf(m, x);
+          }
+        }
+      }
+      if (l == 3 && w == 6) {   // lin4 input = h3 | xyz: rows 445..447 (q 3, g 3, r 1..3) <- x, y, z
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+          const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+          const bool on = g == 3;
+          acc[3][cb][1] = on ? pt.x : acc[3][cb][1];
+          acc[3][cb][2] = on ? pt.y : acc[3][cb][2];
+          acc[3][cb][3] = on ? pt.z : acc[3][cb][3];
+          m = fmaxf(m, on ? fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z))) : 0.f);
+        }
+      }
+      if (!(m < 32768.f)) sm.ovf[p] = it + 1;
+      st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
+      lite_write(acc, 0, sm.H, w, lane);
+      st_signal(&sm.cH[grp]);
+    }
+    {
+      gemm(7);
+      const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      const float usc = ldexpf(1.f, -D.sw[7]);
+      float part[8];
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) part[cb] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 64 * w + 16 * q + 4 * g;
+        const float4 bb = *reinterpret_cast<const float4*>(sm.bias[7] + n0);
+        const float4 w8 = *reinterpret_cast<const float4*>(sm.w8 + n0);
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+            part[cb] = __builtin_fmaf(fetch4(w8, r), v, part[cb]);
+          }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        float s = part[cb];
+        s += xor_lane(s, lane, 16);
+        s += xor_lane(s, lane, 32);
+        if (g == 0) sm.red[w * LTILE + 16 * cb + c] = s;
+      }
+      st_signal(&sm.cH[grp]);
+    }
+    // ---- tanh + classification (B's waves 4, 5), then B's tile-done event
+    if (grp == 1) {
+      const int lane = opaque(threadIdx.x & 63);
+      if (w < 6) {
+        st_wait(&sm.cH[0], 4 * (8 * it + 8), &sm.broken);
+        st_wait(&sm.cH[1], 4 * (8 * it + 8), &sm.broken);
+        const int tid = opaque(threadIdx.x) - 256;
+        if (tid < tl.count) {
+          float s = sm.red[tid];
+          for (int k = 1; k < NWAVE; ++k) s += sm.red[k * LTILE + tid];
+          float y = tanhf(s + D.b8);
+          const float4 pt = *reinterpret_cast<const float4*>(xyz + tid * 4);
+          if (pt.x != pt.x || pt.y != pt.y || pt.z != pt.z || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
+            y = __builtin_nanf("");
+          const int idx = __float_as_int(pt.w);
+          const float margin = E.st[tl.obj].lite_margin;
+          dense[d.cand_off + idx] = y;
+          if (sm.ovf[p] == it + 1 || sm.broken) E.refine[d.cand_off + idx] = 1;     // range guard
+          else if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;          // certainly full
+          else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;        // band (or NaN)
+        }
+      }
+      st_signal(&sm.cE);
+    }
   }
 }
 

@@ -536,3 +536,35 @@ def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
     assert st.lite == 1 and st.refine_points > 0 and st.refine_launches > 0
     assert 0.0 < st.lite_max_err < 0.005 / 4           # 4x inside the smallest margin
     assert abs(st.lite_min_margin - 0.005) < 1e-7      # floor reached after calibration
+
+
+@pytest.mark.gpu
+def test_refine_stops_at_ray_termination(gpu_decoder, monkeypatch):
+    """k_refine_compact skips band samples behind a ray's first certainly-full sample (their
+    transmittance is exactly 0): results bitwise those of refining every band sample
+    (DSR_REFINE_ALL=1), with fewer samples re-decoded."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    monkeypatch.setenv("DSR_LITE", "1")
+    sig = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DSR_REFINE_ALL", mode)
+        h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
+        try:
+            outs = (L.ObjectOut * 8)()
+            ctx.check(lib.dsr_batch_run(h), "run")
+            ctx.check(lib.dsr_batch_download(h, outs), "download")
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+            rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
+                           np.float32)
+            sig[mode] = (rec, st.refine_points, st.fwd_points, st.jac_points)
+        finally:
+            lib.dsr_batch_destroy(h)
+    assert np.array_equal(sig["0"][0], sig["1"][0])
+    assert sig["0"][2:] == sig["1"][2:]
+    assert 0 < sig["0"][1] < sig["1"][1]

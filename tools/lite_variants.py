@@ -49,7 +49,7 @@ for r in range(a.rounds):
         ctx.check(lib.dsr_batch_stats(batch, C.byref(st)), "stats")
         res[v].append((st.fwd_ms / max(1, st.fwd_launches), st.fwd_ms, st.total_ms,
                        2 * bench.FWD_MAC * st.fwd_points / (st.fwd_ms * 1e-3) / 1e12, st.fwd_points,
-                       st.refine_ms, st.jac_ms))
+                       st.refine_ms, st.jac_ms, st.refine_points))
         if v in a.variants:
             sig = np.array([list(outs[i].t_cam_obj) + list(outs[i].code) + [outs[i].loss]
                             for i in range(a.objects)], np.float32)
@@ -61,6 +61,6 @@ for v in allv:
     x = np.median(np.array(res[v]), axis=0)
     tag = "diag" if v in a.diag else ("DIFFERS" if v in bad else "bitwise-equal")
     print(f"{a.var}={v}: lite {x[0]:6.3f} ms/launch {x[1]:7.2f} ms/run {x[3]:7.1f} TF | exact band "
-          f"{x[5]:6.2f} ms | jac {x[6]:6.2f} ms | total {x[2]:7.2f} ms | pts {int(x[4])}  [{tag}]", flush=True)
+          f"{x[5]:6.2f} ms | jac {x[6]:6.2f} ms | total {x[2]:7.2f} ms | pts {int(x[4])} refine {int(x[7])}  [{tag}]", flush=True)
 if bad:
     sys.exit(1)
