@@ -86,12 +86,15 @@ static JacKernel jac_kernel() {
   return k_mlp_jac;
 }
 // Lite-pass variant (DSR_LITE_VARIANT, dsr_mlp_lite.hpp: lite_gemm): 16/32/48 = A ring of
-// 2/3/4 k steps, +8 static activation scale, +64 ring carried across layers (default 88);
-// 18 is a timing experiment (no A streaming)
+// 2/3/4 k steps, +8 static activation scale, +64 ring carried across layers (88), +128
+// staggered wave groups (216: k_mlp_fwd_lite_st, bitwise equal to 88), +256 unscaled lite
+// weights with the bias in the accumulator and a packed fp16 ReLU epilogue (472), +1024
+// swizzled H image (1496, default: 2-way instead of 4-way epilogue store conflicts,
+// bitwise equal to 472); 18 and 984 are timing experiments (invalid results)
 using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                             const float*, float*, ErtArgs);
 #ifndef DSR_DEFAULT_LITE_VARIANT
-#define DSR_DEFAULT_LITE_VARIANT 88
+#define DSR_DEFAULT_LITE_VARIANT 1496
 #endif
 static LiteKernel lite_kernel() {
   const char* e = getenv("DSR_LITE_VARIANT");
@@ -103,9 +106,12 @@ static LiteKernel lite_kernel() {
     case 48: return k_mlp_fwd_lite<true, 48>;
     case 56: return k_mlp_fwd_lite<true, 56>;
     case 24: return k_mlp_fwd_lite<true, 24>;
-    case 216: return k_mlp_fwd_lite_st<true, 88>;     // 88 + staggered groups (bit7)
+    case 88: return k_mlp_fwd_lite<true, 88>;
+    case 216: return k_mlp_fwd_lite_st<true, 88>;
+    case 984: return k_mlp_fwd_lite_st<true, 88 + 256 + 512>;
+    case 472: return k_mlp_fwd_lite_st<true, 88 + 256>;
   }
-  return k_mlp_fwd_lite<true, 88>;
+  return k_mlp_fwd_lite_st<true, 88 + 256 + 1024>;
 }
 // DSR_REFINE_ALL=1: the exact pass re-decodes every band sample, also those behind a ray's
 // first certainly-full sample (k_refine_compact)
@@ -348,6 +354,27 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
     std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
     hf16[l] = add(std::move(as_f));
   }
+  // lite-pass fragments: fp16(W) without the 2^sw scale, so the lite epilogue needs no
+  // rescale multiply (same lane layout as pack_frag16's hi pieces, packed densely)
+  int hl16[8] = {-1};
+  for (int l = 1; l <= 7; ++l) {
+    const int K = (l == 4) ? 448 : 512, T = K / 32;
+    std::vector<_Float16> v16((size_t)32 * T * 64 * 8);
+    for (int rb = 0; rb < 32; ++rb)
+      for (int t = 0; t < T; ++t)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int r = 16 * rb + (lane & 15), c = 32 * t + 8 * (lane >> 4) + j;
+            float x;
+            if (l == 3) x = r < L3_OUT ? Wat(3, r, c) : 0.f;
+            else if (l == 4) x = c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
+            else x = Wat(l, r, c);
+            v16[(((size_t)rb * T + t) * 64 + lane) * 8 + j] = (_Float16)x;
+          }
+    std::vector<float> as_f((v16.size() + 1) / 2);
+    std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
+    hl16[l] = add(std::move(as_f));
+  }
   for (int l = 1; l <= 7; ++l) {
     std::vector<float> v;
     if (l == 3) {
@@ -443,6 +470,7 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   D.b8 = B[8][0];
   for (int l = 0; l < 8; ++l) {
     D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
+    D.Wl_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hl16[l])) : nullptr;
     D.sw[l] = sw16[l];
     D.Wbh_raw[l] = reinterpret_cast<const _Float16*>(P(hb16[l]));
     D.swb[l] = swb16[l];

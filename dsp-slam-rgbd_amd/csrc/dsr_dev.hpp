@@ -49,6 +49,9 @@ struct DevDecoder {
   // [32 rb][K/32][2 pieces (hi, lo)][64 lanes] x 8 halfs, scaled by 2^sw[l]
   const _Float16* Wh_raw[8];
   int sw[8];
+  // lite-pass copies (dsr_mlp_lite.hpp, LV bit8): fp16(W) unscaled, hi pieces only,
+  // [32 rb][K/32][64 lanes] x 8 halfs
+  const _Float16* Wl_raw[8];
   // split-fp16 backward A-fragments of lin_l^T (l = 1..7; [0] = lin0^T, 80 rows), scale 2^swb[l]
   const _Float16* Wbh_raw[8];
   int swb[8];

@@ -1209,12 +1209,26 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ int piv[NPAR];
   __shared__ int flag;
   const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
-  for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {   // tile partials, fp64 combine
-    double a = 0.0, b = 0.0;
-    for (int t = 0; t < ns; ++t) a += (double)slots[(size_t)(d.slot_sdf + t) * SLOT_FLOATS + e];
-    for (int t = 0; t < nk; ++t) b += (double)slots[(size_t)(d.slot_sdf + ns + t) * SLOT_FLOATS + e];
-    Ss[e] = (float)a;
-    Sr[e] = (float)b;
+  {   // tile partials, fp64 combine in tile order; a thread's SPT elements load together
+    constexpr int SPT = (SLOT_FLOATS + SOLVE_THREADS - 1) / SOLVE_THREADS;
+    double a[SPT], b[SPT];
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) a[j] = b[j] = 0.0;
+    const float* s0 = slots + (size_t)d.slot_sdf * SLOT_FLOATS + tid;
+    for (int t = 0; t < ns; ++t, s0 += SLOT_FLOATS)
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+        if (tid + j * SOLVE_THREADS < SLOT_FLOATS) a[j] += (double)s0[j * SOLVE_THREADS];
+    for (int t = 0; t < nk; ++t, s0 += SLOT_FLOATS)
+#pragma unroll
+      for (int j = 0; j < SPT; ++j)
+        if (tid + j * SOLVE_THREADS < SLOT_FLOATS) b[j] += (double)s0[j * SOLVE_THREADS];
+#pragma unroll
+    for (int j = 0; j < SPT; ++j)
+      if (tid + j * SOLVE_THREADS < SLOT_FLOATS) {
+        Ss[tid + j * SOLVE_THREADS] = (float)a[j];
+        Sr[tid + j * SOLVE_THREADS] = (float)b[j];
+      }
   }
   if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
   __syncthreads();

@@ -121,17 +121,24 @@ struct NoHook {
   __device__ __forceinline__ void operator()(int) const {}
 };
 
+// LV bit8 (lite_e2): A fragments from the dense unscaled lite copy (D.Wl_raw: 1 KiB per
+// row block and k step instead of the split layout's 2 KiB stride) and the first step's C
+// operand is `ci` (this wave's bias rows) instead of zero, so the epilogue adds no bias.
 template <bool PRIO, int T, int LV, class Hook = NoHook>
 __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* Wn, int Tn, int w,
                                             const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4],
-                                            int lane, Hook hook = Hook{}) {
-  const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
+                                            int lane, Hook hook = Hook{}, const floatx4* ci = nullptr) {
+  constexpr int WS = (LV & 256) ? 1 : 2;     // KiB per (row block, k step)
+  const _Float16* base = Wl + (size_t)(4 * w) * T * WS * 64 * 8;
   const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * WS * 1024, 0x00020000);
   const int voff = lane * 16;
-  const _Float16* B = H + (lane & 15) * PH + 8 * (lane >> 4);
+  // LV bit10: H image swizzled — 16-B chunk index bit 0 XOR point bit 2 (lite_swz), a
+  // per-lane base offset here
+  const int gsw = (LV & 1024) ? ((lane >> 4) ^ (((lane & 15) >> 2) & 1)) : (lane >> 4);
+  const _Float16* B = H + (lane & 15) * PH + 8 * gsw;
   auto lda = [&](int q, int t) {
-    return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (q * T + t) * 2048, 0));
+    return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (q * T + t) * WS * 1024, 0));
   };
   auto ldb = [&](int cb, int k32) { return *reinterpret_cast<const half8*>(B + cb * 16 * PH + k32); };
   half8 b[4];
@@ -150,9 +157,12 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
     for (int cb = 0; cb < 8; ++cb) {
       b[(cb + 3) & 3] = (cb + 3 < 8) ? ldb(cb + 3, pc) : ldb(cb - 5, pn);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-            a[j][q], b[cb & 3], decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb], 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        floatx4 c0 = floatx4{0.f, 0.f, 0.f, 0.f};
+        if constexpr ((LV & 256) != 0) c0 = ci[q];
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[j][q], b[cb & 3],
+                                                            decltype(FIRST)::value ? c0 : acc[q][cb], 0, 0, 0);
+      }
     }
     if (PRIO) __builtin_amdgcn_s_setprio(0);
   };
@@ -164,10 +174,10 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
   }
   {   // the next matrix's first step, into the slot step T-2 released
     const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<_Float16*>(Wn + (size_t)(4 * w) * Tn * 2 * 64 * 8), 0, 4 * Tn * 2 * 1024, 0x00020000);
+        const_cast<_Float16*>(Wn + (size_t)(4 * w) * Tn * WS * 64 * 8), 0, 4 * Tn * WS * 1024, 0x00020000);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      a[0][q] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, q * Tn * 2048, 0));
+      a[0][q] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rn, voff, q * Tn * WS * 1024, 0));
   }
   step(std::integral_constant<int, 1>{}, std::false_type{}, T - 1);
 }
@@ -175,9 +185,9 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
 template <bool PRIO, int LV, class Hook = NoHook>
 __device__ __forceinline__ void lite_gemm_x(const _Float16* Wl, int T, const _Float16* Wn, int Tn, int w,
                                             const _Float16* H, floatx4 (&acc)[4][8], half8 (&a)[2][4], int lane,
-                                            Hook hook = Hook{}) {
-  if (T != 14) gemm_lite_x<PRIO, 16, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook);
-  else gemm_lite_x<PRIO, 14, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook);
+                                            Hook hook = Hook{}, const floatx4* ci = nullptr) {
+  if (T != 14) gemm_lite_x<PRIO, 16, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook, ci);
+  else gemm_lite_x<PRIO, 14, LV>(Wl, Wn, Tn, w, H, acc, a, lane, hook, ci);
 }
 
 // LV (DSR_LITE_VARIANT): bits 4-5 = NB - 1 (ring depth; 0 is read as NB 2), bit3 static
@@ -216,8 +226,15 @@ __device__ __forceinline__ int lite_scale(float m, float* wmax, int* ovf, int w,
   }
 }
 
+// H swizzle (LV bit10): element (point p, k) at p * PH + (k ^ (8 * ((p >> 2) & 1))).  The
+// 16-lane groups of the epilogue's 8-byte stores (one 4-row slice, 16 points at the 264-dword
+// pitch) hit each bank 4 times unswizzled and twice swizzled; the 16-byte B reads stay
+// conflict-free (their lane groups mix the two slices).  Only a per-lane offset changes.
+__device__ __forceinline__ int lite_swz_g(int g, int c, bool swz) { return swz ? (g ^ (((c >> 2) & 1) << 1)) : g; }
+
+template <bool SWZ = false>
 __device__ __forceinline__ void lite_write(floatx4 (&acc)[4][8], int s, _Float16* H, int w, int lane) {
-  const int g = lane >> 4, c = lane & 15;
+  const int c = lane & 15, g = lite_swz_g(lane >> 4, c, SWZ);
   const float sc = ldexpf(1.f, s);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -467,6 +484,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
   const int grp = w >> 2;
   const int nt = *n_tiles;
   const int lag = E.lag;
+  constexpr bool E2 = (LV & 256) != 0;
+  constexpr int WS = E2 ? 1 : 2;
+  const _Float16* const* WA = E2 ? D.Wl_raw : D.Wh_raw;
   half8 ring[2][4];
   {
     const int tid = opaque(threadIdx.x);
@@ -477,13 +497,13 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
     }
     if (tid < 18) (&sm.ovf[0])[tid] = 0;
     const int lane = tid & 63;
-    const _Float16* A1 = D.Wh_raw[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * 2 * 64 * 8;
+    const _Float16* A1 = WA[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * WS * 64 * 8;
     const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<_Float16*>(A1), 0, 4 * (D.Kf[1] / 32) * 2 * 1024, 0x00020000);
+        const_cast<_Float16*>(A1), 0, 4 * (D.Kf[1] / 32) * WS * 1024, 0x00020000);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       ring[0][q] = __builtin_bit_cast(
-          half8, __builtin_amdgcn_raw_buffer_load_b128(r1, lane * 16, q * (D.Kf[1] / 32) * 2048, 0));
+          half8, __builtin_amdgcn_raw_buffer_load_b128(r1, lane * 16, q * (D.Kf[1] / 32) * WS * 1024, 0));
   }
   __syncthreads();                       // the only block-wide barrier
   int it = 0;
@@ -526,7 +546,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float a = fetch4(bb, r) + ((wx[3 * r] * pt.x + wx[3 * r + 1] * pt.y) + wx[3 * r + 2] * pt.z);
+            const float a =
+                E2 ? __builtin_fmaf(wx[3 * r + 2], pt.z,
+                                    __builtin_fmaf(wx[3 * r + 1], pt.y, __builtin_fmaf(wx[3 * r], pt.x, fetch4(bb, r))))
+                   : fetch4(bb, r) + ((wx[3 * r] * pt.x + wx[3 * r + 1] * pt.y) + wx[3 * r + 2] * pt.z);
             const float h = fmaxf(a, 0.f);
             acc[q][cb][r] = h;
             m = fmaxf(m, h);
@@ -535,7 +558,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
       st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * 7 * it, &sm.broken);   // readers of lin7's input
-      lite_write(acc, 0, sm.H, w, lane);
+      lite_write<(LV & 1024) != 0>(acc, 0, sm.H, w, lane);
       st_signal(&sm.cH[grp]);
     }
     // ---- lin1..lin7 (lin7: + relu, lin8 dot product -> red)
@@ -553,14 +576,64 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         if (t == lag && grp == 0) st_signal(&sm.cP);
       };
       const int ln = l < 7 ? l + 1 : 1;  // (after lin7: the next tile's lin1 fragments)
-      lite_gemm_x<PRIO, LV>(D.Wh_raw[l], D.Kf[l] / 32, D.Wh_raw[ln], D.Kf[ln] / 32, w, sm.H, acc, ring,
-                            opaque(threadIdx.x & 63), hook);
+      floatx4 ci[4];                     // E2: this wave's bias rows start the accumulators
+      if constexpr (E2) {
+        const int g = opaque(threadIdx.x & 63) >> 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ci[q] = *reinterpret_cast<const floatx4*>(sm.bias[l] + 64 * w + 16 * q + 4 * g);
+      }
+      lite_gemm_x<PRIO, LV>(WA[l], D.Kf[l] / 32, WA[ln], D.Kf[ln] / 32, w, sm.H, acc, ring,
+                            opaque(threadIdx.x & 63), hook, ci);
       st_signal(&sm.cRhi);
     };
 #pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
       gemm(l);
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
+      if constexpr (E2) {   // acc = b + W.h already: range max, fp16 convert, packed fp16 ReLU
+        // The range max runs on the bit patterns (signed int order = float order for x >= 0,
+        // every negative below 0, NaN above +inf so it trips the guard): v_max3_i32, no NaN
+        // canonicalisation of the MFMA results that a float max would insert.
+        half4 hv[4][8];
+        int mi = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            const floatx4 v = acc[q][cb];
+            mi = max(mi, max(__float_as_int(v[0]), __float_as_int(v[1])));
+            mi = max(mi, max(__float_as_int(v[2]), __float_as_int(v[3])));
+            half4 h;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (_Float16)v[r];
+            hv[q][cb] = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
+          }
+        if (l == 3 && w == 6) {   // lin4 input rows 445..447 <- x, y, z (after the ReLU)
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+            const bool on = g == 3;
+            hv[3][cb][1] = on ? (_Float16)pt.x : hv[3][cb][1];
+            hv[3][cb][2] = on ? (_Float16)pt.y : hv[3][cb][2];
+            hv[3][cb][3] = on ? (_Float16)pt.z : hv[3][cb][3];
+            mi = max(mi, on ? __float_as_int(fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z)))) : 0);
+          }
+        }
+        if (!(__int_as_float(mi) < 32768.f)) sm.ovf[p] = it + 1;
+        st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            if constexpr ((LV & 512) != 0)   // timing experiment (invalid results): conflict-free stores
+              *reinterpret_cast<half4*>(sm.H + (cb * 4 + q) * 2048 + w * 256 + lane * 4) = hv[q][cb];
+            else
+              *reinterpret_cast<half4*>(sm.H + (16 * cb + c) * PH + 64 * w + 16 * q +
+                                        4 * lite_swz_g(g, c, (LV & 1024) != 0)) = hv[q][cb];
+          }
+        st_signal(&sm.cH[grp]);
+        continue;
+      }
       const float usc = ldexpf(1.f, -D.sw[l]);
       const float* bias = sm.bias[l];
       float m = 0.f;
@@ -590,7 +663,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
       st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
-      lite_write(acc, 0, sm.H, w, lane);
+      lite_write<(LV & 1024) != 0>(acc, 0, sm.H, w, lane);
       st_signal(&sm.cH[grp]);
     }
     {
@@ -609,7 +682,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float v = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+            const float v = E2 ? __int_as_float(max(__float_as_int(accr(acc[q][cb], r)), 0))  // ReLU on bits
+                               : fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
             part[cb] = __builtin_fmaf(fetch4(w8, r), v, part[cb]);
           }
       }

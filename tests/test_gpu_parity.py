@@ -568,3 +568,37 @@ def test_refine_stops_at_ray_termination(gpu_decoder, monkeypatch):
     assert np.array_equal(sig["0"][0], sig["1"][0])
     assert sig["0"][2:] == sig["1"][2:]
     assert 0 < sig["0"][1] < sig["1"][1]
+
+
+@pytest.mark.gpu
+def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
+    """The staggered-group lite kernel (DSR_LITE_VARIANT=216: LDS event counters instead of
+    block barriers, dsr_mlp_lite.hpp: k_mlp_fwd_lite_st) runs the same MFMAs in the same k
+    order as the barrier kernel (88): results bitwise equal, for several stagger lags."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    monkeypatch.setenv("DSR_LITE", "1")
+    sig = {}
+    for v, lag in (("88", "4"), ("216", "0"), ("216", "4"), ("216", "7")):
+        monkeypatch.setenv("DSR_LITE_VARIANT", v)
+        monkeypatch.setenv("DSR_LITE_LAG", lag)
+        h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
+        try:
+            outs = (L.ObjectOut * 8)()
+            ctx.check(lib.dsr_batch_run(h), "run")
+            ctx.check(lib.dsr_batch_download(h, outs), "download")
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+            rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
+                           np.float32)
+            sig[(v, lag)] = (rec, st.fwd_points, st.refine_points, st.jac_points)
+        finally:
+            lib.dsr_batch_destroy(h)
+    ref = sig[("88", "4")]
+    for k, s in sig.items():
+        assert np.array_equal(s[0].view(np.uint32), ref[0].view(np.uint32)), k
+        assert s[1:] == ref[1:], k

@@ -1,7 +1,7 @@
 """A/B kernel variants (an env switch: DSR_LITE_VARIANT, DSR_SPLIT_RING, ...) in ONE process,
 interleaved.
 
-Usage (GPU box): python tools/lite_variants.py 16 24 [--var DSR_LITE_VARIANT] [--diag 18] [--rounds 5] [--iters 1]
+Usage (GPU box): python tools/lite_variants.py 16 24 [--var DSR_LITE_VARIANT | DSR_RENDER_PASSES ...] [--diag 18] [--rounds 5] [--iters 1]
 Each run is a batch of `--iters` GN iterations over 64 KITTI-like objects.  Prints the median
 lite-kernel ms per launch and TFLOP/s (one fp16 product per MAC), and checks that every
 non-diagnostic variant returns results bitwise equal to the first one (the variants only change
@@ -24,8 +24,8 @@ from reconstruct import _libdsr as L  # noqa: E402
 import bench  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("variants", nargs="*", type=int, default=[0])
-ap.add_argument("--diag", nargs="*", type=int, default=[])
+ap.add_argument("variants", nargs="*", default=["0"])
+ap.add_argument("--diag", nargs="*", default=[])
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--objects", type=int, default=64)
 ap.add_argument("--iters", type=int, default=1)
@@ -33,16 +33,20 @@ ap.add_argument("--var", default="DSR_LITE_VARIANT")
 a = ap.parse_args()
 dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS)
 cfg = dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=a.iters))
-batch, keep = bench.make_batch(dec, L.optim_params(cfg), a.objects, 1000)
 lib, ctx = dec.ctx.lib, dec.ctx
 outs = (L.ObjectOut * a.objects)()
 allv = list(a.variants) + list(a.diag)
 res = {v: [] for v in allv}
+batches = {}
+for v in allv:     # one batch per variant: switches read at batch creation (DSR_RENDER_PASSES) apply too
+    os.environ[a.var] = str(v)
+    batches[v] = bench.make_batch(dec, L.optim_params(cfg), a.objects, 1000)
 ref = None
 bad = []
 for r in range(a.rounds):
     for v in allv:
         os.environ[a.var] = str(v)
+        batch = batches[v][0]
         ctx.check(lib.dsr_batch_run(batch), "run")
         ctx.check(lib.dsr_batch_download(batch, outs), "dl")
         st = L.Stats()
