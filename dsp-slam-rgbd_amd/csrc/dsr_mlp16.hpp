@@ -39,6 +39,16 @@ struct Fwd16Shared {
 };
 
 // one 32-k step of the 3-product MFMA block for a 64x64 wave tile
+// Hh/Hl images are swizzled: element (point p, k) at p * PH + (k ^ (8 * ((p >> 2) & 1))).
+// Unswizzled, the 16-lane groups of write_split's 8-byte stores (16 points of one 4-row
+// slice at the 264-dword pitch) hit every bank 4 times; swizzled twice, and the 16-byte B
+// reads stay conflict-free (their lane groups mix the two slices).  Readers: the lane's
+// B base offset below; writer: write_split.
+__device__ __forceinline__ int h_boff(int lane) {
+  const int c = lane & 15;
+  return c * PH + 8 * ((lane >> 4) ^ ((c >> 2) & 1));
+}
+
 template <bool PRIO, int NQ, int EX = 0>
 __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&al)[NQ], const half8 (&bh)[4],
                                            const half8 (&bl)[4], floatx4 (&acc)[NQ][4]) {
@@ -92,7 +102,7 @@ __device__ __forceinline__ void gemm16_tile_x(const half8* __restrict__ A, int T
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const int boff = h_boff(lane);
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
   half8 ah1[NQ], al1[NQ], bh0[4], bl0[4], bh1[4], bl1[4];
@@ -141,7 +151,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
   for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) acc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const int boff = h_boff(lane);
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
   half8 ah0[NQ], al0[NQ], ah1[NQ], al1[NQ], bh0[4], bl0[4], bh1[4], bl1[4];
@@ -191,7 +201,7 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
   const int voff = lane * 16;
-  const int boff = (lane & 15) * PH + 8 * (lane >> 4);
+  const int boff = h_boff(lane);
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
   auto lda = [&](int q, int t, int piece) {
@@ -288,10 +298,10 @@ __device__ __forceinline__ int block_scale(float m, float* wmax, int w, int lane
 }
 
 // Write the wave's 64x64 block of fp32 activations (acc layout, v[q][cb][r]) as hi/lo
-// fp16 pieces scaled by 2^s.
+// fp16 pieces scaled by 2^s (swizzled image, h_boff).
 __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _Float16* Hh, _Float16* Hl,
                                             int w, int lane) {
-  const int g = lane >> 4, c = lane & 15;
+  const int c = lane & 15, g = (lane >> 4) ^ (((c >> 2) & 1) << 1);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n0 = 64 * w + 16 * q + 4 * g;
