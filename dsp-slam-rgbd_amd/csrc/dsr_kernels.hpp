@@ -1207,6 +1207,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ float jrot[NPOSE];
   __shared__ float scal[4];
   __shared__ int piv[NPAR];
+  __shared__ float pivv[NPAR];
   __shared__ int flag;
   const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
   {   // tile partials, fp64 combine in tile order; a thread's SPT elements load together
@@ -1214,15 +1215,30 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     double a[SPT], b[SPT];
 #pragma unroll
     for (int j = 0; j < SPT; ++j) a[j] = b[j] = 0.0;
+    // (4 tiles' loads in flight per step: the partials were just written by the Jacobian
+    // kernel and come from L2/MALL, so a step is one memory latency)
     const float* s0 = slots + (size_t)d.slot_sdf * SLOT_FLOATS + tid;
-    for (int t = 0; t < ns; ++t, s0 += SLOT_FLOATS)
+    auto acc_tiles = [&](double (&x)[SPT], int n) {
+      int t = 0;
+      for (; t + 4 <= n; t += 4, s0 += 4 * SLOT_FLOATS) {
+        float v[4][SPT];
 #pragma unroll
-      for (int j = 0; j < SPT; ++j)
-        if (tid + j * SOLVE_THREADS < SLOT_FLOATS) a[j] += (double)s0[j * SOLVE_THREADS];
-    for (int t = 0; t < nk; ++t, s0 += SLOT_FLOATS)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int j = 0; j < SPT; ++j)
-        if (tid + j * SOLVE_THREADS < SLOT_FLOATS) b[j] += (double)s0[j * SOLVE_THREADS];
+          for (int j = 0; j < SPT; ++j)
+            v[u][j] = (tid + j * SOLVE_THREADS < SLOT_FLOATS) ? s0[u * SLOT_FLOATS + j * SOLVE_THREADS] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < SPT; ++j) x[j] += (double)v[u][j];
+      }
+      for (; t < n; ++t, s0 += SLOT_FLOATS)
+#pragma unroll
+        for (int j = 0; j < SPT; ++j)
+          if (tid + j * SOLVE_THREADS < SLOT_FLOATS) x[j] += (double)s0[j * SOLVE_THREADS];
+    };
+    acc_tiles(a, ns);
+    acc_tiles(b, nk);
 #pragma unroll
     for (int j = 0; j < SPT; ++j)
       if (tid + j * SOLVE_THREADS < SLOT_FLOATS) {
@@ -1302,40 +1318,63 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       trace_H[((size_t)it * stride + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
   }
   __syncthreads();
-  // ---- LU with partial pivoting (torch.inverse, optimizer.py:188)
+  // ---- LU with partial pivoting (torch.inverse, optimizer.py:188): 2 barriers per pivot.
+  // Pivot search of column k: first max |A[r][k]|, r >= k (LAPACK getrf), by wave 0, fused
+  // into the previous step's update of column k.  Per step: (X) row swap + column scale,
+  // (Y) rank-1 update; the arithmetic is getf2's (multiplier by reciprocal, one fma per
+  // element), so the factors are bitwise those of the 4-phase schedule.
+  auto pivot_search = [&](int k, int r0, float v0, int r1, float v1) {   // wave 0, lanes' candidates
+    float best = -1.f, bv = 0.f;
+    int bi = NPAR;
+    if (r0 < NPAR && fabsf(v0) > best) { best = fabsf(v0); bi = r0; bv = v0; }
+    if (r1 < NPAR && fabsf(v1) > best) { best = fabsf(v1); bi = r1; bv = v1; }
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ob = __shfl_xor(best, off), ov = __shfl_xor(bv, off);
+      const int oi = __shfl_xor(bi, off);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; bv = ov; }
+    }
+    if (tid == 0) { piv[k] = bi; pivv[k] = bv; }
+  };
+  if (tid < 64) pivot_search(0, tid, A[tid][0], tid + 64, tid + 64 < NPAR ? A[tid + 64][0] : 0.f);
+  __syncthreads();
   for (int k = 0; k < NPAR; ++k) {
-    if (tid < 64) {
-      float best = -1.f;
-      int bi = NPAR;
-      for (int r = k + tid; r < NPAR; r += 64) {
-        const float v = fabsf(A[r][k]);
-        if (v > best) { best = v; bi = r; }
+    const int p = piv[k];
+    {   // (X) swap rows k, p (every column but k); column k: pivot to the diagonal, scale below
+      const float pv = pivv[k];                            // = A[p][k] (written below)
+      const float rc = 1.0f / pv;
+      for (int c = tid; c < NPAR; c += SOLVE_THREADS)
+        if (c != k && p != k) { const float t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+      for (int r = k + 1 + tid; r < NPAR; r += SOLVE_THREADS) {
+        const float x = (r == p) ? A[k][k] : A[r][k];      // post-swap row r's column-k value
+        A[r][k] = x * rc;
+        if (r == p) A[k][k] = pv;
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        const float ob = __shfl_xor(best, off);
-        const int oi = __shfl_xor(bi, off);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-      }
-      if (tid == 0) piv[k] = bi;
     }
     __syncthreads();
-    const int p = piv[k];
-    if (p != k)
-      for (int c = tid; c < NPAR; c += SOLVE_THREADS) { float t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
-    __syncthreads();
-    const float rc = 1.0f / A[k][k];
-    for (int r = k + 1 + tid; r < NPAR; r += SOLVE_THREADS) A[r][k] = A[r][k] * rc;
-    __syncthreads();
-    const int m = NPAR - k - 1;
-    for (int e = tid; e < m * m; e += SOLVE_THREADS) {
-      const int r = k + 1 + e / m, c = k + 1 + e % m;
-      A[r][c] = __builtin_fmaf(-A[r][k], A[k][c], A[r][c]);
+    {   // (Y) trailing update; wave 0 owns column k+1 and searches its pivot
+      const int m = NPAR - k - 1;
+      if (tid < 64) {
+        if (k + 1 < NPAR) {
+          const int c = k + 1;
+          const int r0 = k + 1 + tid, r1 = r0 + 64;
+          float v0 = 0.f, v1 = 0.f;
+          if (r0 < NPAR) { v0 = __builtin_fmaf(-A[r0][k], A[k][c], A[r0][c]); A[r0][c] = v0; }
+          if (r1 < NPAR) { v1 = __builtin_fmaf(-A[r1][k], A[k][c], A[r1][c]); A[r1][c] = v1; }
+          pivot_search(k + 1, r0, v0, r1, v1);
+        }
+      } else if (m > 1) {
+        const int mc = m - 1;                               // columns k+2 .. NPAR-1
+        for (int e = tid - 64; e < m * mc; e += SOLVE_THREADS - 64) {
+          const int r = k + 1 + e / mc, c = k + 2 + e % mc;
+          A[r][c] = __builtin_fmaf(-A[r][k], A[k][c], A[r][c]);
+        }
+      }
     }
     __syncthreads();
   }
-  // inverse(H) = U^-1 L^-1 P I, all 71 columns at once in LDS: the row permutation of
-  // the identity, then right-looking substitutions (one barrier per pivot row, every
-  // (row, column) pair in parallel; each element accumulates in the column-solve order)
+  // inverse(H) = U^-1 L^-1 P I in LDS: the row permutation of the identity, then the
+  // forward / back substitutions of getrs, one column per thread (each element
+  // accumulates in the column-solve order)
   for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) X[e / NPAR][e % NPAR] = 0.f;
   __syncthreads();
   if (tid == 0) {
@@ -1348,23 +1387,19 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     for (int i = 0; i < NPAR; ++i) X[i][perm[i]] = 1.f;
   }
   __syncthreads();
-  for (int l = 0; l < NPAR - 1; ++l) {    // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
-    const int m = NPAR - 1 - l;
-    for (int e = tid; e < m * NPAR; e += SOLVE_THREADS) {
-      const int i = l + 1 + e / NPAR, c = e % NPAR;
-      X[i][c] = __builtin_fmaf(-A[i][l], X[l][c], X[i][c]);
+  if (tid < NPAR) {   // thread c solves column c alone: no barriers, same per-element order
+    const int c = tid;
+    for (int l = 0; l < NPAR - 1; ++l) {  // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
+      const float xl = X[l][c];
+      for (int i = l + 1; i < NPAR; ++i) X[i][c] = __builtin_fmaf(-A[i][l], xl, X[i][c]);
     }
-    __syncthreads();
-  }
-  for (int i = NPAR - 1; i >= 0; --i) {   // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
-    for (int c = tid; c < NPAR; c += SOLVE_THREADS) X[i][c] = X[i][c] / A[i][i];
-    __syncthreads();
-    for (int e = tid; e < i * NPAR; e += SOLVE_THREADS) {
-      const int r = e / NPAR, c = e % NPAR;
-      X[r][c] = __builtin_fmaf(-A[r][i], X[i][c], X[r][c]);
+    for (int i = NPAR - 1; i >= 0; --i) { // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
+      const float xi = X[i][c] / A[i][i];
+      X[i][c] = xi;
+      for (int r = 0; r < i; ++r) X[r][c] = __builtin_fmaf(-A[r][i], xi, X[r][c]);
     }
-    __syncthreads();
   }
+  __syncthreads();
   if (tid < NPAR) {                     // dx = inverse(H) b
     float s = 0.f;
     for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
