@@ -455,31 +455,36 @@ __global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const O
 
 __global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
                             Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+  // Every object's sdf tiles (forward + backward) first, then every render tile (backward
+  // only, kept masks): the persistent grid's blocks then run tiles of one kind together, so
+  // the layers they stream stay in step (L2-resident weights).  Tile outputs go to slots
+  // derived from the tile itself (jac_tail), so the order changes no result.
   __shared__ int base_s;
   if (threadIdx.x == 0) base_s = 0;
   __syncthreads();
-  for (int o = 0; o < n_obj; ++o) {
-    ObjState& S = st[o];
-    const bool run = S.status == ST_RUNNING;
-    const int ns = run ? desc[o].n_pts : 0;
-    const int nk = run ? S.k : 0;
-    const int ts = (ns + TILE - 1) / TILE, tk = (nk + TILE - 1) / TILE;
-    const int b = base_s;
-    for (int i = threadIdx.x; i < ts + tk; i += blockDim.x) {
-      Tile t;
-      t.obj = o;
-      if (i < ts) { t.term = 0; t.start = i * TILE; t.count = min(TILE, ns - i * TILE); }
-      else { const int j = i - ts; t.term = 1; t.start = j * TILE; t.count = min(TILE, nk - j * TILE); }
-      tiles[b + i] = t;
+  for (int term = 0; term < 2; ++term)
+    for (int o = 0; o < n_obj; ++o) {
+      ObjState& S = st[o];
+      const bool run = S.status == ST_RUNNING;
+      const int n = run ? (term == 0 ? desc[o].n_pts : S.k) : 0;
+      const int tn = (n + TILE - 1) / TILE;
+      const int b = base_s;
+      for (int i = threadIdx.x; i < tn; i += blockDim.x) {
+        Tile t;
+        t.obj = o;
+        t.term = term;
+        t.start = i * TILE;
+        t.count = min(TILE, n - i * TILE);
+        tiles[b + i] = t;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        base_s = b + tn;
+        if (term == 0) S.n_sdf_tiles = tn;
+        else S.n_ren_tiles = tn;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      base_s = b + ts + tk;
-      S.n_sdf_tiles = ts;
-      S.n_ren_tiles = tk;
-    }
-    __syncthreads();
-  }
   if (threadIdx.x == 0) *n_tiles = base_s;
 }
 
