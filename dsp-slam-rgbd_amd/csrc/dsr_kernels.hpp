@@ -430,27 +430,53 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
 // ------------------------------------------------------------------------------------
 // tile tables (single workgroup)
 // ------------------------------------------------------------------------------------
-__global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize) {
-  __shared__ int base_s;
-  if (threadIdx.x == 0) base_s = 0;
+// Tile tables (one block of 1024 threads): a block-wide exclusive scan of the per-object tile
+// counts gives every object its first tile, then each thread writes its object's tiles.
+// Object order, then tile order within an object — the table the serial loop would build.
+template <class Count, class Emit>
+__device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit emit) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+  if (tid == 0) carry = base;
   __syncthreads();
-  for (int o = 0; o < n_obj; ++o) {
-    const ObjState& S = st[o];
-    const int n = (S.status == ST_RUNNING) ? S.n_emit : 0;
-    const int nt = (n + tsize - 1) / tsize;
-    const int b = base_s;
-    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
-      Tile t;
-      t.obj = o; t.term = 0; t.start = i * tsize;
-      t.count = min(tsize, n - i * tsize);
-      tiles[b + i] = t;
+  for (int o0 = 0; o0 < n_obj; o0 += blockDim.x) {
+    const int o = o0 + tid;
+    int n = 0, nt = 0;
+    if (o < n_obj) count(o, n, nt);
+    const int inc = wave_incl_scan(nt, lane);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    if (wv == 0) {
+      int v = lane < nw ? wsum[lane] : 0;
+      v = wave_incl_scan(v, lane);
+      if (lane < nw) wsum[lane] = v;
     }
     __syncthreads();
-    if (threadIdx.x == 0) base_s = b + nt;
+    const int first = carry + (wv ? wsum[wv - 1] : 0) + inc - nt;
+    for (int i = 0; i < nt; ++i) emit(first + i, o, i, n);
+    __syncthreads();
+    if (tid == 0) carry += wsum[nw - 1];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *n_tiles = base_s;
+  return carry;
+}
+
+__global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize) {
+  const int total = tile_scan(
+      n_obj, 0,
+      [&](int o, int& n, int& nt) {
+        n = (st[o].status == ST_RUNNING) ? st[o].n_emit : 0;
+        nt = (n + tsize - 1) / tsize;
+      },
+      [&](int idx, int o, int i, int n) {
+        Tile t;
+        t.obj = o; t.term = 0; t.start = i * tsize;
+        t.count = min(tsize, n - i * tsize);
+        tiles[idx] = t;
+      });
+  if (threadIdx.x == 0) *n_tiles = total;
 }
 
 __global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
@@ -459,33 +485,24 @@ __global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjStat
   // only, kept masks): the persistent grid's blocks then run tiles of one kind together, so
   // the layers they stream stay in step (L2-resident weights).  Tile outputs go to slots
   // derived from the tile itself (jac_tail), so the order changes no result.
-  __shared__ int base_s;
-  if (threadIdx.x == 0) base_s = 0;
-  __syncthreads();
+  int total = 0;
   for (int term = 0; term < 2; ++term)
-    for (int o = 0; o < n_obj; ++o) {
-      ObjState& S = st[o];
-      const bool run = S.status == ST_RUNNING;
-      const int n = run ? (term == 0 ? desc[o].n_pts : S.k) : 0;
-      const int tn = (n + TILE - 1) / TILE;
-      const int b = base_s;
-      for (int i = threadIdx.x; i < tn; i += blockDim.x) {
-        Tile t;
-        t.obj = o;
-        t.term = term;
-        t.start = i * TILE;
-        t.count = min(TILE, n - i * TILE);
-        tiles[b + i] = t;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        base_s = b + tn;
-        if (term == 0) S.n_sdf_tiles = tn;
-        else S.n_ren_tiles = tn;
-      }
-      __syncthreads();
-    }
-  if (threadIdx.x == 0) *n_tiles = base_s;
+    total = tile_scan(
+        n_obj, total,
+        [&](int o, int& n, int& nt) {
+          ObjState& S = st[o];
+          n = (S.status == ST_RUNNING) ? (term == 0 ? desc[o].n_pts : S.k) : 0;
+          nt = (n + TILE - 1) / TILE;
+          if (term == 0) S.n_sdf_tiles = nt;
+          else S.n_ren_tiles = nt;
+        },
+        [&](int idx, int o, int i, int n) {
+          Tile t;
+          t.obj = o; t.term = term; t.start = i * TILE;
+          t.count = min(TILE, n - i * TILE);
+          tiles[idx] = t;
+        });
+  if (threadIdx.x == 0) *n_tiles = total;
 }
 
 // ------------------------------------------------------------------------------------
