@@ -254,6 +254,20 @@ __device__ __forceinline__ float3 ray_sample(const float* __restrict__ rays, con
   const float cx = rays[ray * 3 + 0] * d, cy = rays[ray * 3 + 1] * d, cz = rays[ray * 3 + 2] * d;
   return xform(S.T, cx, cy, cz);
 }
+// The same sample from an LDS copy of the object's depths and pose (SampleLds) and the ray
+// held in registers: the per-sample loop does no global loads.
+struct SampleLds {
+  float T[12];
+  float depths[MAXM];
+};
+__device__ __forceinline__ void stage_samples(SampleLds& L, const ObjState& S, int M, int tid) {
+  if (tid < 12) L.T[tid] = S.T[tid];
+  if (tid < M) L.depths[tid] = S.depths[tid];
+}
+__device__ __forceinline__ float3 ray_sample(const float3 r, const SampleLds& L, int j) {
+  const float d = L.depths[j];
+  return xform(L.T, r.x * d, r.y * d, r.z * d);
+}
 
 // ------------------------------------------------------------------------------------
 // k_sample_pass: the ray samples of loss.py:71-82, emitted in render passes with early
@@ -291,20 +305,24 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
   __shared__ int wsum[SAMPLE_THREADS / 64];
   __shared__ int wnin[SAMPLE_THREADS / 64];
   __shared__ int base_s, nin_s;
+  __shared__ SampleLds L;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) { base_s = 0; nin_s = 0; }
+  stage_samples(L, S, M, tid);
   __syncthreads();
   for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
     const int ray = r0 + tid;
     int cnt = 0, nin = 0;
     bool alive = false;
+    float3 rv = make_float3(0.f, 0.f, 0.f);
     if (ray < d.n_rays) {
+      rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
       if (first) dead[d.ray_off + ray] = 0;
       alive = first || dead[d.ray_off + ray] == 0;
       if (alive) {
         int rank = 0;
         for (int j = 0; j < M; ++j) {
-          const float3 x = ray_sample(rays, S, ray, j);
+          const float3 x = ray_sample(rv, L, j);
           const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
           if (!(nrm < 1.0f)) {                                             // loss.py:82
             if (first) dense[d.cand_off + ray * M + j] = __builtin_nanf("");
@@ -329,7 +347,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
     if (cnt > 0) {
       int rank = 0;
       for (int j = 0; j < M && rank < rb; ++j) {
-        const float3 x = ray_sample(rays, S, ray, j);
+        const float3 x = ray_sample(rv, L, j);
         const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
         if (!(nrm < 1.0f)) continue;
         if (rank >= ra) cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
@@ -387,20 +405,34 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) base_s = 0;
   __syncthreads();
+  __shared__ uint64_t rbits[SAMPLE_THREADS];
+  const float full = nth - S.lite_margin;
   for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
     const int ray = r0 + tid;
-    unsigned char* f = refine + d.cand_off + (size_t)ray * M;
-    uint64_t bits = 0;
-    if (ray < d.n_rays) {
-      const float full = nth - S.lite_margin;
-      const float* y = dense ? dense + d.cand_off + (size_t)ray * M : nullptr;
-      int j = 0;
-      for (; j < M; ++j) {
-        if (f[j]) { bits |= 1ull << j; f[j] = 0; }
-        else if (y && y[j] <= full) { ++j; break; }
+    // Each wave scans 64 rays one at a time, lane j on sample j (coalesced flag / value
+    // loads, ballots): refined = the flagged samples in front of the first unflagged sample
+    // that is certainly full; every flag is cleared.
+    for (int i0 = 0; i0 < 64; i0 += 8) {     // 8 rays' loads in flight
+      unsigned char fv[8];
+      float yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = r0 + 64 * wv + i0 + u;
+        const bool in = rr < d.n_rays && lane < M;
+        const size_t e = d.cand_off + (size_t)rr * M + lane;
+        fv[u] = in ? refine[e] : 0;
+        yv[u] = (in && dense) ? dense[e] : __builtin_nanf("");
       }
-      for (; j < M; ++j) f[j] = 0;          // behind the terminating sample: not refined
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = r0 + 64 * wv + i0 + u;
+        const uint64_t fb = __ballot(fv[u] != 0), ub = __ballot(fv[u] == 0 && yv[u] <= full);
+        const uint64_t b = ub ? (fb & ((1ull << __builtin_ctzll(ub)) - 1)) : fb;
+        if (rr < d.n_rays && lane < M) refine[d.cand_off + (size_t)rr * M + lane] = 0;
+        if (lane == i0 + u) rbits[tid] = b;
+      }
     }
+    const uint64_t bits = rbits[tid];
     const int cnt = __popcll(bits);
     const int inc = wave_incl_scan(cnt, lane);
     if (lane == 63) wsum[wv] = inc;
