@@ -119,8 +119,12 @@ static bool refine_all() {
   const char* e = getenv("DSR_REFINE_ALL");
   return e && atoi(e) != 0;
 }
-// DSR_LITE_LAG (staggered lite kernel): the k step group A reaches before group B starts a GEMM
+// DSR_LITE_LAG (staggered lite kernel): the k step group A reaches before group B starts a GEMM.
+// DSR_LITE_BREAK=1 (test hook): every block starts in the "broken" state of a timed-out
+// event wait, so every sample goes to the exact pass (lag -1)
 static int lite_lag() {
+  const char* b = getenv("DSR_LITE_BREAK");
+  if (b && atoi(b) != 0) return -1;
   const char* e = getenv("DSR_LITE_LAG");
   const int v = e ? atoi(e) : 4;
   return v < 0 ? 0 : (v > 7 ? 7 : v);

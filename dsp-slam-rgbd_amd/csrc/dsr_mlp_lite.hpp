@@ -495,7 +495,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       if (l < 6) sm.bias[l < 3 ? l + 1 : l + 2][n] = D.bias[l < 3 ? l + 1 : l + 2][n];
       else sm.w8[n] = D.W8[n];
     }
-    if (tid < 18) (&sm.ovf[0])[tid] = 0;
+    if (tid < 18) {   // counters and flags; DSR_LITE_BREAK test hook: start broken
+      int* f = &sm.ovf[0] + tid;
+      *f = (f == &sm.broken && E.lag < 0) ? 1 : 0;
+    }
     const int lane = tid & 63;
     const _Float16* A1 = WA[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * WS * 64 * 8;
     const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(

@@ -602,3 +602,36 @@ def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
     for k, s in sig.items():
         assert np.array_equal(s[0].view(np.uint32), ref[0].view(np.uint32)), k
         assert s[1:] == ref[1:], k
+
+
+@pytest.mark.gpu
+def test_lite_broken_block_falls_back_to_exact(gpu_decoder, monkeypatch):
+    """A staggered lite block whose event wait times out marks itself broken and sends every
+    sample it classifies to the exact pass.  Forced on every block (DSR_LITE_BREAK=1), all
+    samples are re-decoded exactly and no ray terminates early on a lite value: results
+    bitwise those of the exact path (DSR_LITE=0; early ray termination is exact)."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    sig = {}
+    for mode in ("exact", "broken"):
+        monkeypatch.setenv("DSR_LITE", "0" if mode == "exact" else "1")
+        monkeypatch.setenv("DSR_LITE_BREAK", "1" if mode == "broken" else "0")
+        h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 4, 1000)
+        try:
+            outs = (L.ObjectOut * 4)()
+            ctx.check(lib.dsr_batch_run(h), "run")
+            ctx.check(lib.dsr_batch_download(h, outs), "download")
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+            rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
+                           np.float32)
+            sig[mode] = (rec, st.jac_points, st.refine_points, st.fwd_points)
+        finally:
+            lib.dsr_batch_destroy(h)
+    assert np.array_equal(sig["broken"][0].view(np.uint32), sig["exact"][0].view(np.uint32))
+    assert sig["broken"][1] == sig["exact"][1]
+    assert sig["broken"][2] == sig["broken"][3] > 0      # every lite-classified sample refined
