@@ -276,7 +276,7 @@ __device__ __forceinline__ int act_scale_exp(float m) {
   if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
   int e;
   (void)frexpf(m, &e);               // m = f 2^e, f in [0.5, 1)
-  return 14 - e;
+  return min(14 - e, 126);           // (a tile whose activations all stay below 2^-112: 2^126)
 }
 
 __device__ __forceinline__ float wave_max(float v, int lane) {
@@ -297,6 +297,9 @@ __device__ __forceinline__ int block_scale(float m, float* wmax, int w, int lane
   return act_scale_exp(mm);
 }
 
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+
 // Write the wave's 64x64 block of fp32 activations (acc layout, v[q][cb][r]) as hi/lo
 // fp16 pieces scaled by 2^s (swizzled image, h_boff).
 __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _Float16* Hh, _Float16* Hl,
@@ -309,12 +312,16 @@ __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _F
     for (int cb = 0; cb < 4; ++cb) {
       const int p = 16 * cb + c;
       half4 hh, hl;
+      // 2^s is a normal float (act_scale_exp keeps s in [-114, 126]): x * 2^s == ldexp(x, s);
+      // in pairs (v_pk_mul_f32, v_cvt_pk_f16_f32, v_pk_add_f32)
+      const float2v sc2 = float2v{1.f, 1.f} * ldexpf(1.f, s);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float x = ldexpf(v[q][cb][r], s);
-        const _Float16 h = (_Float16)x;
-        hh[r] = h;
-        hl[r] = (_Float16)(x - (float)h);
+      for (int r = 0; r < 4; r += 2) {
+        const float2v x = float2v{v[q][cb][r], v[q][cb][r + 1]} * sc2;
+        const half2v h = __builtin_convertvector(x, half2v);
+        const half2v l = __builtin_convertvector(x - __builtin_convertvector(h, float2v), half2v);
+        hh[r] = h[0]; hh[r + 1] = h[1];
+        hl[r] = l[0]; hl[r + 1] = l[1];
       }
       *reinterpret_cast<half4*>(Hh + p * PH + n0) = hh;
       *reinterpret_cast<half4*>(Hl + p * PH + n0) = hl;
