@@ -236,7 +236,8 @@ def main():
         split_peak = FP32_MFMA_PEAK_TF
         split_note = "fp32 MFMA dense peak"
     if lite:
-        kernel, kname = "k_mlp_fwd_lite", "k_mlp_fwd_lite (one-product fp16 classification pass over ray samples)"
+        kernel, kname = ("k_mlp_fwd_lite_st",
+                         "k_mlp_fwd_lite_st (one-product fp16 classification pass over ray samples)")
         peak_tf, peak_note = FP16_MFMA_PEAK_TF, "dense fp16 MFMA peak (one product per MAC, fp32 accumulate)"
     else:
         kernel, kname = "k_mlp_fwd16", "k_mlp_fwd16 (decode_sdf on ray samples, 3xFP16)"
