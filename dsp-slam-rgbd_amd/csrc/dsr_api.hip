@@ -185,6 +185,7 @@ struct dsr_batch {
   float *tr_H = nullptr, *tr_v = nullptr;
   int* tr_i = nullptr;
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
+  int* rinfo = nullptr;         // per-ray in-ball run (first in-ball sample | count << 8), or -1
   unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
   MaskArgs ma{nullptr, nullptr, nullptr, nullptr};   // kept masks of the exact re-decode
   int* kslot = nullptr;
@@ -631,6 +632,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->kpts, sizeof(float4) * (size_t)cand_off);
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
+  ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
   {
     const char* e = getenv("DSR_LITE");
     b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1);
@@ -815,7 +817,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead);
+                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
                            b->lite ? LTILE : TILE);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));

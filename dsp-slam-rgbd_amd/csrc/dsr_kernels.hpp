@@ -295,7 +295,8 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
                                                                 ObjState* st, const float* __restrict__ rays_all,
                                                                 int M, int ra, int rb, float4* __restrict__ cand,
-                                                                float* __restrict__ dense, int* __restrict__ dead) {
+                                                                float* __restrict__ dense, int* __restrict__ dead,
+                                                                int* __restrict__ rinfo) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -314,13 +315,22 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
     const int ray = r0 + tid;
     int cnt = 0, nin = 0;
     bool alive = false;
+    int j0 = -1;                  // later passes: the ray's in-ball samples are j0 .. j0+nin-1
     float3 rv = make_float3(0.f, 0.f, 0.f);
     if (ray < d.n_rays) {
       rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
       if (first) dead[d.ray_off + ray] = 0;
       alive = first || dead[d.ray_off + ray] == 0;
-      if (alive) {
-        int rank = 0;
+      if (alive && !first) {
+        const int info = rinfo[d.ray_off + ray];
+        if (info >= 0) {          // contiguous in-ball run (first pass): the window directly
+          j0 = info & 255;
+          nin = info >> 8;
+          cnt = max(0, min(rb, nin) - ra);
+        }
+      }
+      if (alive && j0 < 0) {
+        int rank = 0, jf = -1, jl = -1;
         for (int j = 0; j < M; ++j) {
           const float3 x = ray_sample(rv, L, j);
           const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
@@ -328,11 +338,17 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
             if (first) dense[d.cand_off + ray * M + j] = __builtin_nanf("");
             continue;
           }
+          if (jf < 0) jf = j;
+          jl = j;
           if (rank >= ra && rank < rb) ++cnt;
           ++rank;
           if (!first && rank >= rb) break;
         }
         nin = rank;
+        // the in-ball set of a ray is one run of samples unless rounding makes |x| < 1
+        // flicker near a tangent point; such rays keep scanning in every pass
+        if (first)
+          rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
       }
     }
     const int inc = wave_incl_scan(cnt, lane);
@@ -344,7 +360,12 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
     __syncthreads();
     int off = base_s + inc - cnt;
     for (int k = 0; k < wv; ++k) off += wsum[k];
-    if (cnt > 0) {
+    if (cnt > 0 && j0 >= 0) {
+      for (int k = ra; k < ra + cnt; ++k) {
+        const float3 x = ray_sample(rv, L, j0 + k);
+        cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j0 + k));
+      }
+    } else if (cnt > 0) {
       int rank = 0;
       for (int j = 0; j < M && rank < rb; ++j) {
         const float3 x = ray_sample(rv, L, j);
