@@ -815,6 +815,8 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
       const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
+      DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
+                                       (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);

@@ -273,7 +273,8 @@ __device__ __forceinline__ float3 ray_sample(const float3 r, const SampleLds& L,
 // k_sample_pass: the ray samples of loss.py:71-82, emitted in render passes with early
 // ray termination.  Pass [ra, rb) emits, for every ray not yet flagged dead, its
 // in-ball samples of in-ball rank ra..rb-1 (rank = position among the ray's in-ball
-// samples, depth order).  A ray is flagged dead by the fwd kernel when one of its samples
+// samples, depth order).  `dense` is NaN-filled before the first pass (out-of-ball samples
+// stay NaN; samples behind a terminated ray are never read).  A ray is flagged dead by the fwd kernel when one of its samples
 // decodes to sdf <= -th: its occupancy is then exactly 1 (0.5 - (-th)/(2 th), loss_utils.py
 // :46-47), the cumulative transmittance exactly 0 from there on (loss.py:111), so every
 // later sample of the ray enters d_u, var_u and de_do (loss.py:112-132) multiplied by an
@@ -334,10 +335,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
         for (int j = 0; j < M; ++j) {
           const float3 x = ray_sample(rv, L, j);
           const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
-          if (!(nrm < 1.0f)) {                                             // loss.py:82
-            if (first) dense[d.cand_off + ray * M + j] = __builtin_nanf("");
-            continue;
-          }
+          if (!(nrm < 1.0f)) continue;   // loss.py:82 (out of ball: NaN, dense pre-filled)
           if (jf < 0) jf = j;
           jl = j;
           if (rank >= ra && rank < rb) ++cnt;
