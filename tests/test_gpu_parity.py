@@ -635,3 +635,23 @@ def test_lite_broken_block_falls_back_to_exact(gpu_decoder, monkeypatch):
     assert np.array_equal(sig["broken"][0].view(np.uint32), sig["exact"][0].view(np.uint32))
     assert sig["broken"][1] == sig["exact"][1]
     assert sig["broken"][2] == sig["broken"][3] > 0      # every lite-classified sample refined
+
+
+def test_large_batch_tile_tables(gpu_decoder, monkeypatch):
+    """Batches of more than 1024 objects: the block-scan tile tables (k_tiles_fwd/_jac,
+    tile_scan) cross their 1024-object chunks; objects on both sides of the boundary match
+    their one-by-one runs bitwise."""
+    monkeypatch.setenv("DSR_STREAMS", "1")
+    opt = _opt(gpu_decoder, dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
+                                                                    num_iterations=2)), "Redwood")
+    objs = []
+    for i in range(1100):
+        o = S.make_object(5000 + i, n_pts=40 + (i % 7), n_bg=8, scale=1.0, tz=3.0, upright=False)
+        objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
+    batch, tr = opt.reconstruct_objects(objs, trace=True)
+    for i in (0, 1, 1023, 1024, 1025, 1099):
+        single, tr1 = opt.reconstruct_objects([objs[i]], trace=True)
+        assert batch[i]["is_good"] == single[0]["is_good"], i
+        assert batch[i]["loss"] == single[0]["loss"], i
+        for key in ("H", "b", "n_valid", "k"):
+            assert np.array_equal(tr[i][key], tr1[0][key]), (i, key)
