@@ -25,6 +25,10 @@
 #include "dsr_mlp_lite.hpp"
 #include "../../include/dsr.h"
 
+// wave-wide 64-bit max (ockl DPP reduction; declared by HIP only under
+// HIP_ENABLE_EXTRA_WARP_SYNC_TYPES)
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_max_u64(unsigned long long);
+
 namespace dsr {
 
 // ------------------------------------------------------------------------------------
@@ -1253,10 +1257,20 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
   }
 }
 
+// lane k (a constant after unrolling) of every quad, to the whole quad (DPP quad_perm)
+__device__ __forceinline__ float quad_bcast(float v, int k) {
+  switch (k) {
+    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x00, 0xf, 0xf, false));
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x55, 0xf, 0xf, false));
+    case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xaa, 0xf, 0xf, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xff, 0xf, 0xf, false));
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // k_solve: optimizer.py:131-194 for one object per workgroup
 // ------------------------------------------------------------------------------------
-constexpr int SOLVE_THREADS = 256;
+constexpr int SOLVE_THREADS = 320;   // 5 waves: substitutions run 4 lanes per column
 constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render, T, z
 
 // trace_* hold [iteration][stride objects]; the pointers are pre-offset to this launch's
@@ -1283,6 +1297,9 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ float pivv[NPAR];
   __shared__ int flag;
   const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
+#ifdef DSR_SOLVE_PROFILE
+  const long long tp0 = wall_clock64();
+#endif
   {   // tile partials, fp64 combine in tile order; a thread's SPT elements load together
     constexpr int SPT = (SLOT_FLOATS + SOLVE_THREADS - 1) / SOLVE_THREADS;
     double a[SPT], b[SPT];
@@ -1391,22 +1408,30 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       trace_H[((size_t)it * stride + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
   }
   __syncthreads();
+#ifdef DSR_SOLVE_PROFILE
+  const long long tp1 = wall_clock64();
+#endif
   // ---- LU with partial pivoting (torch.inverse, optimizer.py:188): 2 barriers per pivot.
   // Pivot search of column k: first max |A[r][k]|, r >= k (LAPACK getrf), by wave 0, fused
   // into the previous step's update of column k.  Per step: (X) row swap + column scale,
   // (Y) rank-1 update; the arithmetic is getf2's (multiplier by reciprocal, one fma per
   // element), so the factors are bitwise those of the 4-phase schedule.
+  // One 64-bit key per candidate: |v| bits (order-preserving for |v| >= 0) over 0xffff - row
+  // (ties: the first row); NaN rows key 0, never chosen (fabsf(NaN) > best is false).  The
+  // wave max (DPP reduction) is the first max; its signed value is read back from A, which
+  // wave 0 wrote before (LDS keeps a wave's accesses in order).
   auto pivot_search = [&](int k, int r0, float v0, int r1, float v1) {   // wave 0, lanes' candidates
-    float best = -1.f, bv = 0.f;
-    int bi = NPAR;
-    if (r0 < NPAR && fabsf(v0) > best) { best = fabsf(v0); bi = r0; bv = v0; }
-    if (r1 < NPAR && fabsf(v1) > best) { best = fabsf(v1); bi = r1; bv = v1; }
-    for (int off = 32; off > 0; off >>= 1) {
-      const float ob = __shfl_xor(best, off), ov = __shfl_xor(bv, off);
-      const int oi = __shfl_xor(bi, off);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; bv = ov; }
+    auto key = [](float v, int r) -> unsigned long long {
+      const float a = fabsf(v);
+      return (r < NPAR && a >= 0.f) ? ((unsigned long long)__float_as_uint(a) << 32) | (unsigned)(0xffff - r) : 0ull;
+    };
+    const unsigned long long k0 = key(v0, r0), k1 = key(v1, r1);
+    const unsigned long long km = __ockl_wfred_max_u64(k0 > k1 ? k0 : k1);
+    if (tid == 0) {
+      const int bi = km ? 0xffff - (int)(km & 0xffffffffull) : NPAR;
+      piv[k] = bi;
+      pivv[k] = bi < NPAR ? A[bi][k] : 0.f;
     }
-    if (tid == 0) { piv[k] = bi; pivv[k] = bv; }
   };
   if (tid < 64) pivot_search(0, tid, A[tid][0], tid + 64, tid + 64 < NPAR ? A[tid + 64][0] : 0.f);
   __syncthreads();
@@ -1445,6 +1470,9 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     }
     __syncthreads();
   }
+#ifdef DSR_SOLVE_PROFILE
+  const long long tp2 = wall_clock64();
+#endif
   // inverse(H) = U^-1 L^-1 P I in LDS: the row permutation of the identity, then the
   // forward / back substitutions of getrs, one column per thread (each element
   // accumulates in the column-solve order)
@@ -1460,17 +1488,38 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     for (int i = 0; i < NPAR; ++i) X[i][perm[i]] = 1.f;
   }
   __syncthreads();
-  if (tid < NPAR) {   // thread c solves column c alone: no barriers, same per-element order
-    const int c = tid;
-    for (int l = 0; l < NPAR - 1; ++l) {  // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
-      const float xl = X[l][c];
-      for (int i = l + 1; i < NPAR; ++i) X[i][c] = __builtin_fmaf(-A[i][l], xl, X[i][c]);
+  // Column c is solved by the 4 lanes 4c..4c+3 of one wave, lane `sub` holding rows
+  // i = sub + 4m (m < 18) in registers; a pivot row's value reaches the quad by a DPP
+  // broadcast, A is read as LDS broadcasts.  No barriers; each element is updated by one
+  // lane in the column-solve order (bitwise the getrs substitutions).
+  if (tid < 4 * NPAR) {
+    const int c = tid >> 2, sub = tid & 3;
+    constexpr int NM = (NPAR + 3) / 4;
+    float x[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) x[m] = (sub + 4 * m < NPAR) ? X[sub + 4 * m][c] : 0.f;
+#pragma unroll
+    for (int l = 0; l < NPAR - 1; ++l) {   // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
+      const float xl = quad_bcast(x[l >> 2], l & 3);
+#pragma unroll
+      for (int m = l / 4; m < NM; ++m) {
+        const int i = sub + 4 * m;
+        if (i > l && i < NPAR) x[m] = __builtin_fmaf(-A[i][l], xl, x[m]);
+      }
     }
-    for (int i = NPAR - 1; i >= 0; --i) { // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
-      const float xi = X[i][c] / A[i][i];
-      X[i][c] = xi;
-      for (int r = 0; r < i; ++r) X[r][c] = __builtin_fmaf(-A[r][i], xi, X[r][c]);
+#pragma unroll
+    for (int i = NPAR - 1; i >= 0; --i) {  // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
+      const float xi = quad_bcast(x[i >> 2], i & 3) / A[i][i];
+      if (sub == (i & 3)) x[i >> 2] = xi;
+#pragma unroll
+      for (int m = 0; 4 * m < i; ++m) {
+        const int r = sub + 4 * m;
+        if (r < i) x[m] = __builtin_fmaf(-A[r][i], xi, x[m]);
+      }
     }
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+      if (sub + 4 * m < NPAR) X[sub + 4 * m][c] = x[m];
   }
   __syncthreads();
   if (tid < NPAR) {                     // dx = inverse(H) b

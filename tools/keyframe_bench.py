@@ -5,7 +5,8 @@ Usage (GPU box): python tools/keyframe_bench.py [--objects 8] [--reps 20]
 """
 import argparse, os, sys, time
 import numpy as np
-sys.path.insert(0, "dsp-slam-rgbd_amd"); sys.path.insert(0, ".")
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "dsp-slam-rgbd_amd")); sys.path.insert(0, REPO)
 import synthetic as S
 from deep_sdf.workspace import decoder_from_state
 from reconstruct import _libdsr as L
