@@ -681,6 +681,13 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
     float du = 0.f, dob = 0.f;
     uint64_t keep = 0;
     const float* sd = dense + d.cand_off + (size_t)ray * M;
+    {   // the round's sdf rows, coalesced, into the transmittance rows (each scan reads
+        // sample j before overwriting it with T_j); the per-ray scans then wait on LDS only
+      const int nr = min(RENDER_THREADS, d.n_rays - r0);
+      const float* src = dense + d.cand_off + (size_t)r0 * M;
+      for (int e = tid; e < nr * M; e += RENDER_THREADS) T_s[(e / M) * (MAXM + 1) + e % M] = src[e];
+      __syncthreads();
+    }
     if (ray < d.n_rays) {
       // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
       // probabilities and rendered depth (:112-125).  The 51-term sum is accumulated in
@@ -694,7 +701,7 @@ __global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjD
       double dud = 0.0;
       int j = 0;
       for (; j < M && T != 0.f; ++j) {
-        const float s = sd[j];
+        const float s = Tr[j];                       // = sd[j] (staged above)
         const float ov = occupancy(s, nth, th, two_th);
         if (s > nth && s < th) grad |= 1ull << j;     // loss.py:101
         const float tp = ov * T;
