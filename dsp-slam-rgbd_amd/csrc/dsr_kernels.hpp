@@ -1467,11 +1467,12 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
           if (r1 < NPAR) { v1 = __builtin_fmaf(-A[r1][k], A[k][c], A[r1][c]); A[r1][c] = v1; }
           pivot_search(k + 1, r0, v0, r1, v1);
         }
-      } else if (m > 1) {
-        const int mc = m - 1;                               // columns k+2 .. NPAR-1
-        for (int e = tid - 64; e < m * mc; e += SOLVE_THREADS - 64) {
-          const int r = k + 1 + e / mc, c = k + 2 + e % mc;
-          A[r][c] = __builtin_fmaf(-A[r][k], A[k][c], A[r][c]);
+      } else if (m > 1) {         // rows k+1.., columns k+2..: a fixed 16 x 16 thread grid
+        static_assert(SOLVE_THREADS - 64 == 256, "trailing-update grid");
+        const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15;
+        for (int r = k + 1 + rr; r < NPAR; r += 16) {
+          const float ark = A[r][k];
+          for (int c = k + 2 + cc; c < NPAR; c += 16) A[r][c] = __builtin_fmaf(-ark, A[k][c], A[r][c]);
         }
       }
     }
@@ -1529,6 +1530,10 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       if (sub + 4 * m < NPAR) X[sub + 4 * m][c] = x[m];
   }
   __syncthreads();
+#ifdef DSR_SOLVE_PROFILE                 // (tools: per-phase wall clock of block 0, 100 MHz ticks)
+  const long long tp3 = wall_clock64();
+  if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2);
+#endif
   if (tid < NPAR) {                     // dx = inverse(H) b
     float s = 0.f;
     for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
