@@ -1,17 +1,25 @@
 """Benchmark: object-reconstructions/sec (2048 pts, 10 GN iters) on N MI355X.
 
 One "step" = one full ``reconstruct_object`` (10 joint GN iterations, KITTI
-parameters, configs/config_kitti.json:21-39) for every object of this rank's
-batch: 64 synthetic KITTI-like objects x 2048 surface points x (2048+200) rays
-per GPU (BASELINE.json north-star "2048 pts/object x 64 objects on 1 MI355X"),
-plus the device->host copy of the results and, for N>1, one RCCL all-gather of
-the fixed-size result records.  Objects are independent, so the
-batch is sharded across ranks with no data-path collective: weak scaling.
+parameters, configs/config_kitti.json:21-39) for every object of the job: by default
+64 synthetic KITTI-like objects x 2048 surface points x (2048+200) rays (BASELINE.json
+north star "2048 pts/object x 64 objects on 1 MI355X"), plus the device->host copy of
+the results and, for N>1, one RCCL all-gather of the fixed-size result records
+(SURVEY.md §8e).
 
-Inputs are resident in HBM before the timed region (dsr_batch_create); each
-step re-initialises the optimizer state on device and runs all iterations.
+Scaling: the job is FIXED (64 objects) and LPT-sharded across the N ranks
+(reconstruct/parallel.py: ResidentShard) — strong scaling, the north star's
+"≥6x strong scaling to 8 GPUs"; at N=1 this is exactly the metric's configuration.
+``--weak`` instead gives every rank its own 64 objects.  ``--pts 4096`` is BASELINE
+config 4 (64 objects x 4096 points, 8 per GPU at N=8).
 
-Usage: python bench.py [--gpus N --steps K --warmup W --objects B]
+Inputs are resident in HBM before the timed region (dsr_batch_create); each step
+re-initialises the optimizer state on device and runs all iterations.  At N=1 rank 0
+also reports: the exact-decode leg (``value_exact``: DSR_LITE=0, every ray sample
+decoded in 3xFP16), the three MFMA kernels' rooflines, the CPU baseline, and the
+Redwood keyframe leg (BASELINE config 5, ``keyframe``).
+
+Usage: python bench.py [--gpus N --steps K --warmup W --objects B --pts P --weak]
        (N>1 through torch.distributed.run, one process per GPU)
 """
 from __future__ import annotations
@@ -33,20 +41,22 @@ import synthetic as S  # noqa: E402
 
 FWD_MAC = 1_769_984     # algorithmic forward MACs / point (code broadcast folded), SURVEY §8
 BWD_MAC = 1_835_520     # input-gradient backward MACs / point
-FP32_MFMA_PEAK_TF = 157.3
-FP16_MFMA_PEAK_TF = 2500.0          # dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+FP16_MFMA_PEAK_TF = 2500.0          # dense fp16/bf16 MFMA, spec (MI355X_MICROARCH.md)
+FP16_MFMA_LOOP_TF = 1247.0          # the guide's bare bf16 MFMA loop on random data (DVFS item 1)
 SPLIT_PRODUCTS = 3                  # 3xFP16: hi*hi + hi*lo + lo*hi per fp32 product
-
+DTYPE = ("fp16-mfma: 3xFP16 split (hi/lo fp16, fp32 accumulate) for every value that reaches "
+         "an output + one-product fp16 classification of ray samples")
 
 LAST_CREATE_S = None
 
 
-def make_batch(dec, opt_params, n_obj, base_seed):
+def make_batch(dec, opt_params, n_obj, base_seed, n_pts=2048):
+    """Resident batch of ``n_obj`` KITTI-like objects (seeds base_seed + i)."""
     from reconstruct import _libdsr as L
 
     keep, ins = [], (L.ObjectIn * n_obj)()
     for i in range(n_obj):
-        o = S.kitti_object(i, base_seed=base_seed)
+        o = S.kitti_object(i, base_seed=base_seed, n_pts=n_pts)
         arrs = [np.ascontiguousarray(a, np.float32) for a in (o.pts, o.rays, o.depth)]
         keep += arrs
         r = L.ObjectIn()
@@ -67,7 +77,7 @@ def make_batch(dec, opt_params, n_obj, base_seed):
     return h, keep
 
 
-def cpu_baseline(seconds_budget=30.0):
+def cpu_baseline(seconds_budget=30.0, n_pts=2048):
     """The CPU oracle (numpy, all host threads) on a bounded sample of the workload."""
     from deep_sdf.workspace import fold_state
     from oracle import dsr_oracle as O
@@ -75,7 +85,7 @@ def cpu_baseline(seconds_budget=30.0):
     state = S.make_decoder(1234)
     dec = O.Decoder(fold_state(state, S.DEFAULT_SPECS))
     P = O.OptimParams.from_cfg(S.KITTI_OPTIM)
-    o = S.kitti_object(0)
+    o = S.kitti_object(0, n_pts=n_pts)
     t0 = time.time()
     # one metric-unit object, 10 GN iterations (stop early past the budget and extrapolate)
     n_fg = o.depth.shape[0]
@@ -100,18 +110,18 @@ def cpu_baseline(seconds_budget=30.0):
     threads = int(os.environ.get("OMP_NUM_THREADS", cores))
     return {"value": 1.0 / per_obj, "unit": "object-reconstructions/sec", "cores": min(threads, cores),
             "kind": "port",
-            "sample": f"oracle/dsr_oracle.py (numpy fp32) on 1 KITTI object x 2048 pts, {done} of "
+            "sample": f"oracle/dsr_oracle.py (numpy fp32) on 1 KITTI object x {n_pts} pts, {done} of "
                       f"{P.num_iterations} GN iterations timed ({dt:.1f} s), extrapolated to 10"}
 
 
-def pmc_traffic(kernel="k_mlp_fwd16"):
+def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_summary.json, written by tools/prof_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes over this same default workload), or None."""
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json"))):   # tag order r1 < r1b < ...
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json"))):   # tag order
         try:
             d = json.load(open(f))
         except Exception:
@@ -122,13 +132,103 @@ def pmc_traffic(kernel="k_mlp_fwd16"):
     return best
 
 
+def stats_sum(acc, st):
+    for k, _ in st._fields_:
+        v = getattr(st, k)
+        if k in ("lite_max_err",):
+            acc[k] = max(acc.get(k, 0.0), v)
+        elif k in ("lite_min_margin",):
+            acc[k] = min(acc.get(k, 1e30), v)
+        elif k in ("lite", "keep_masks", "pad_"):
+            acc[k] = v
+        else:
+            acc[k] = acc.get(k, 0) + v
+    return acc
+
+
+def kernel_rooflines(a):
+    """Per-launch rate of the three MFMA kernels over the timed steps (HIP events on the
+    stream each kernel runs on, dsr_batch_stats) against the spec peak and the guide's
+    measured bare-MFMA-loop rate.  FLOPs are algorithmic and EXECUTED: the lite pass one
+    fp16 product per MAC; the exact re-decode and the Jacobian fp32-equivalent (a 3xFP16
+    MAC counts once, the spec peak is divided by 3); render points with kept ReLU masks
+    run the backward chain only."""
+    out = {}
+    split_peak, split_loop = FP16_MFMA_PEAK_TF / SPLIT_PRODUCTS, FP16_MFMA_LOOP_TF / SPLIT_PRODUCTS
+    ren_mac = BWD_MAC if a.get("keep_masks") else FWD_MAC + BWD_MAC
+
+    def entry(name, flop, ms, launches, peak, loop, note):
+        tf = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        out[name] = {"achieved_tflops": round(tf, 2), "peak_tflops": round(peak, 1),
+                     "frac_of_peak": round(tf / peak, 4), "bare_mfma_loop_tflops": round(loop, 1),
+                     "frac_of_bare_loop": round(tf / loop, 4), "launches": launches,
+                     "avg_launch_ms": round(ms / max(1, launches), 5),
+                     "flop_per_launch": flop / max(1, launches), "flop_counted": note}
+
+    if a.get("lite"):
+        entry("k_mlp_fwd_lite_st", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
+              FP16_MFMA_PEAK_TF, FP16_MFMA_LOOP_TF, "2*1,769,984 per decoded ray sample, fp16 products")
+        entry("k_mlp_fwd16 (exact re-decode: band + audit)", 2.0 * FWD_MAC * a["refine_points"],
+              a["refine_ms"], a["refine_launches"], split_peak, split_loop,
+              "2*1,769,984 per re-decoded sample, fp32-equivalent (3xFP16)")
+    else:
+        entry("k_mlp_fwd16", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
+              split_peak, split_loop, "2*1,769,984 per decoded ray sample, fp32-equivalent (3xFP16)")
+    jflop = 2.0 * (FWD_MAC + BWD_MAC) * a["jac_surface_points"] + 2.0 * ren_mac * a["jac_render_points"]
+    entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop,
+          "N surface points x 2*(1,769,984+1,835,520) + K render points x 2*"
+          + ("1,835,520 (backward only, kept masks)" if a.get("keep_masks") else "(fwd+bwd)"))
+    return out
+
+
+def keyframe_leg(dec, n_keyframes=6, objects=4):
+    """BASELINE config 5: Redwood parameters, per keyframe `objects` new detections, each
+    also run as its flipped hypothesis (LocalMapping_util.cc:394-410), 512 points, 5 GN
+    iterations — one batched asynchronous call per keyframe
+    (Optimizer.reconstruct_keyframe_async), so the host is free for the reference's
+    LocalBundleAdjustment (LocalMapping.cc:99-128) while the GPU works.  Reports ms per
+    keyframe (uploads included) and the host time spent while batches were in flight."""
+    from reconstruct.optimizer import Optimizer
+    from reconstruct.utils import ForceKeyErrorDict
+
+    opt = Optimizer(dec, ForceKeyErrorDict(data_type="Redwood", optimizer=S.REDWOOD_OPTIM))
+    kfs = []
+    for k in range(n_keyframes):
+        dets = []
+        for i in range(objects):
+            o = S.redwood_object(100 * k + i)
+            dets.append((o.t_cam_obj, o.pts, o.rays, o.depth, None, False))
+        kfs.append(dets)
+    opt.reconstruct_keyframe(kfs[0])                  # warm-up
+    t0 = time.perf_counter()
+    host_s = 0.0
+    good = 0
+    for dets in kfs:
+        h = opt.reconstruct_keyframe_async(dets)
+        t1 = time.perf_counter()
+        while not h.done():                           # stand-in for host-side BA
+            pass
+        host_s += time.perf_counter() - t1
+        good += sum(r["is_good"] for r in h.wait())
+    dt = time.perf_counter() - t0
+    return {"keyframes": n_keyframes, "detections_per_keyframe": objects,
+            "objects_per_keyframe_batch": 2 * objects,
+            "ms_per_keyframe": round(dt / n_keyframes * 1e3, 3), "good_detections": good,
+            "host_free_ms_per_keyframe": round(host_s / n_keyframes * 1e3, 3),
+            "note": "Redwood params, 512 pts, 712 rays, 5 iters; original + flipped hypothesis per "
+                    "detection in one async batch (includes H2D upload and result download)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--objects", type=int, default=64, help="objects per GPU")
+    ap.add_argument("--objects", type=int, default=64, help="objects in the job (per GPU with --weak)")
+    ap.add_argument("--pts", type=int, default=2048, help="surface points per object (config 4: 4096)")
+    ap.add_argument("--weak", action="store_true", help="every rank its own --objects objects")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the exact-decode and keyframe legs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,8 +238,9 @@ def main():
     # DSR_BENCH_BACKEND=gloo (host tensors) rehearses the N>1 code path with several ranks on
     # one device, which RCCL refuses; the driver's runs use RCCL ("nccl") over xGMI
     backend = os.environ.get("DSR_BENCH_BACKEND", "nccl")
+    import torch
+
     if world > 1:
-        import torch
         import torch.distributed as dist
 
         if backend == "nccl":
@@ -148,105 +249,59 @@ def main():
         else:
             dist.init_process_group(backend)
             local = local % max(1, torch.cuda.device_count())
-    coll_dev = "cuda" if backend == "nccl" else "cpu"
+    coll_dev = torch.device("cuda", local) if backend == "nccl" and world > 1 else None
 
     from deep_sdf.workspace import decoder_from_state
     from reconstruct import _libdsr as L
+    from reconstruct.optimizer import Optimizer
+    from reconstruct.parallel import ResidentShard
+    from reconstruct.utils import ForceKeyErrorDict
 
     state = S.make_decoder(1234)
     dec = decoder_from_state(state, S.DEFAULT_SPECS, device=local)
-    params = L.optim_params(S.KITTI_OPTIM)
-    n_obj = args.objects
-    batch, keep = make_batch(dec, params, n_obj, base_seed=1000 + rank * 100000)
+    opt = Optimizer(dec, ForceKeyErrorDict(data_type="KITTI", optimizer=S.KITTI_OPTIM))
+    n_job = args.objects * (world if args.weak else 1)
+    objs = []
+    for i in range(n_job):
+        o = S.kitti_object(i, base_seed=1000, n_pts=args.pts)
+        objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
+    t0 = time.perf_counter()
+    shard = ResidentShard(opt, objs, device=coll_dev)
+    create_s = time.perf_counter() - t0
     lib, ctx = dec.ctx.lib, dec.ctx
-    outs = (L.ObjectOut * n_obj)()
-    rec = np.zeros((n_obj, 96), np.float32)
 
-    def step():
-        ctx.check(lib.dsr_batch_run(batch), "dsr_batch_run")
-        ctx.check(lib.dsr_batch_download(batch, outs), "dsr_batch_download")
-        for i in range(n_obj):
-            o = outs[i]
-            rec[i, :16] = o.t_cam_obj
-            rec[i, 16:80] = o.code
-            rec[i, 80] = o.loss
-            rec[i, 81] = o.is_good
+    def barrier():
         if dist is not None:
-            import torch
-
-            t = torch.from_numpy(rec).to(coll_dev)
-            gath = torch.empty((world * n_obj, 96), dtype=torch.float32, device=t.device)
-            dist.all_gather_into_tensor(gath, t)       # RCCL over xGMI
-            torch.cuda.synchronize()
+            dist.barrier()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step()
-    if dist is not None:
-        import torch
-
-        dist.barrier()
-        torch.cuda.synchronize()
-    ctx.check(lib.dsr_batch_sync(batch), "sync")
-    t0 = time.perf_counter()
-    fwd_ms = jac_ms = 0.0
-    fwd_pts = jac_pts = inball_pts = fwd_launches = 0
-    refine_ms, refine_pts, lite_err, lite_margin, lite = 0.0, 0, 0.0, 1e30, False
+        shard.run()
+    barrier()
+    acc = {}
     n_good = 0
+    t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        st = L.Stats()
-        ctx.check(lib.dsr_batch_stats(batch, C.byref(st)), "stats")
-        fwd_ms += st.fwd_ms
-        jac_ms += st.jac_ms
-        fwd_pts += st.fwd_points
-        jac_pts += st.jac_points
-        inball_pts += st.inball_points
-        fwd_launches += st.fwd_launches
-        refine_ms += st.refine_ms
-        refine_pts += st.refine_points
-        lite_err = max(lite_err, st.lite_max_err)
-        lite_margin = min(lite_margin, st.lite_min_margin)
-        lite = bool(st.lite)
-        n_good += sum(int(outs[i].is_good) for i in range(n_obj))
-    ctx.check(lib.dsr_batch_sync(batch), "sync")
-    if dist is not None:
-        import torch
-
-        torch.cuda.synchronize()
-        dist.barrier()
+        res = shard.run()
+        if shard.handle is not None:
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(shard.handle, C.byref(st)), "stats")
+            stats_sum(acc, st)
+        if res is not None:
+            n_good += sum(int(r["is_good"]) for r in res)
+    barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev or "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_obj = n_obj * world * args.steps
-    value = total_obj / elapsed
-    fwd_flop = 2.0 * FWD_MAC * fwd_pts
-    jac_flop = 2.0 * (FWD_MAC + BWD_MAC) * jac_pts
-    fwd_tf = fwd_flop / (fwd_ms * 1e-3) / 1e12 if fwd_ms > 0 else 0.0
-    job_tf = (fwd_flop + jac_flop) / elapsed / 1e12
-    variant = int(os.environ.get("DSR_FWD_VARIANT", "12"))
-    if variant & 8:
-        split_peak = FP16_MFMA_PEAK_TF / SPLIT_PRODUCTS
-        split_note = ("fp32-equivalent peak of the 3xFP16 split: 2.5 PF dense fp16 MFMA / 3 products; "
-                      "achieved counts algorithmic fp32 FLOPs (executed fp16 MFMA FLOPs = 3x)")
-    else:
-        split_peak = FP32_MFMA_PEAK_TF
-        split_note = "fp32 MFMA dense peak"
-    if lite:
-        kernel, kname = ("k_mlp_fwd_lite_st",
-                         "k_mlp_fwd_lite_st (one-product fp16 classification pass over ray samples)")
-        peak_tf, peak_note = FP16_MFMA_PEAK_TF, "dense fp16 MFMA peak (one product per MAC, fp32 accumulate)"
-    else:
-        kernel, kname = "k_mlp_fwd16", "k_mlp_fwd16 (decode_sdf on ray samples, 3xFP16)"
-        peak_tf, peak_note = split_peak, split_note
-    refine_flop = 2.0 * FWD_MAC * refine_pts
-    refine_tf = refine_flop / (refine_ms * 1e-3) / 1e12 if refine_ms > 0 else 0.0
+    value = n_job * args.steps / elapsed
+    roof = kernel_rooflines(acc) if acc else {}
     if rank == 0:
+        dom = "k_mlp_fwd_lite_st" if acc.get("lite") else "k_mlp_fwd16"
+        r = roof.get(dom, {})
         out = {
-            "metric": "object-reconstructions/sec (2048 pts, 10 GN iters)",
+            "metric": f"object-reconstructions/sec ({args.pts} pts, 10 GN iters)",
             "value": value,
             "unit": "object-reconstructions/sec",
             "n_gpus": world,
@@ -254,51 +309,68 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": None,
-            "dtype": "f32",
-            "mfma_precision": ("ray samples classified by a one-product fp16 pass; every value that "
-                               "reaches an output (band samples, Jacobian points) decoded in 3xFP16 split "
-                               "(hi/lo fp16, fp32 accumulate; fp32-class, parity suite green)") if lite else
-                              ("3xFP16 split (hi/lo fp16 pieces, power-of-2 scaled, fp32 accumulate; "
-                               "fp32-class accuracy, parity suite green)") if variant & 8 else "fp32 MFMA",
+            "dtype": DTYPE,
             "data": "synthetic (seeded DeepSDF 8x512 decoder + KITTI-like objects, SURVEY.md §8d)",
-            "config": {"workload": f"{n_obj} objects/GPU x 2048 pts x (2048+200) rays x 50 depth "
-                                   "samples, 10 GN iters, KITTI params (BASELINE configs[1] unit, "
-                                   "batched as north-star 64 objects/GPU)",
-                       "objects_per_gpu": n_obj, "pts": 2048, "rays": 2248, "iters": 10,
-                       "parallelism": f"object-sharded x{world}"},
-            "roofline": {"bound": "mfma", "kernel": kname,
-                         "achieved": round(fwd_tf, 3), "peak": round(peak_tf, 1),
-                         "unit": "TFLOP/s", "frac": round(fwd_tf / peak_tf, 4),
-                         "peak_note": peak_note,
+            "config": {"workload": f"{n_job} objects x {args.pts} pts x ({args.pts}+200) rays x 50 depth "
+                                   "samples, 10 GN iters, KITTI params (BASELINE configs[1] unit; "
+                                   + ("64 objects per GPU)" if args.weak else
+                                      f"one {n_job}-object job LPT-sharded over {world} GPU(s))"),
+                       "objects": n_job, "objects_on_rank0": len(shard.mine), "pts": args.pts,
+                       "rays": args.pts + 200, "iters": 10,
+                       "parallelism": f"object-sharded x{world}" + (" (weak)" if args.weak else " (strong)")},
+            "roofline": {"bound": "mfma", "kernel": dom,
+                         "achieved": r.get("achieved_tflops"), "peak": r.get("peak_tflops"),
+                         "unit": "TFLOP/s", "frac": r.get("frac_of_peak"),
                          "traffic": None, "traffic_unit": "bytes/launch (HBM+MALL, PMC)",
-                         "launches": fwd_launches,
-                         "flop_per_launch": fwd_flop / max(1, fwd_launches),
-                         "avg_launch_ms": fwd_ms / max(1, fwd_launches)},
-            "early_ray_termination": {"samples_decoded": fwd_pts, "samples_in_ball": inball_pts,
-                                      "decoded_fraction": round(fwd_pts / max(1, inball_pts), 4)},
-            "lite_pass": None if not lite else {
-                "refine_points": refine_pts, "refine_fraction": round(refine_pts / max(1, fwd_pts), 4),
-                "refine_kernel": "k_mlp_fwd16 (3xFP16)", "refine_ms_per_step": refine_ms / args.steps,
-                "refine_tflops": round(refine_tf, 3), "refine_peak": round(split_peak, 1),
-                "max_observed_lite_error": lite_err, "min_margin": lite_margin},
-            "job_tflops": round(job_tf, 3),
-            "jac_kernel_tflops": round(jac_flop / (jac_ms * 1e-3) / 1e12, 3) if jac_ms > 0 else 0.0,
-            "good_fraction": n_good / float(n_obj * args.steps),
-            # inputs handed over in host memory: dsr_batch_create's upload added to one step
-            "host_inclusive_value": n_obj * world / (elapsed / args.steps + LAST_CREATE_S),
-            "batch_create_ms": LAST_CREATE_S * 1e3,
+                         "avg_launch_ms": r.get("avg_launch_ms"), "launches": r.get("launches"),
+                         "flop_per_launch": r.get("flop_per_launch")},
+            "rooflines": roof,
+            "early_ray_termination": {"samples_decoded": acc.get("fwd_points"),
+                                      "samples_in_ball": acc.get("inball_points"),
+                                      "decoded_fraction": round(acc.get("fwd_points", 0)
+                                                                / max(1, acc.get("inball_points", 1)), 4)},
+            "lite_pass": None if not acc.get("lite") else {
+                "refine_points": acc["refine_points"], "audit_points": acc["audit_points"],
+                "refine_fraction": round(acc["refine_points"] / max(1, acc["fwd_points"]), 4),
+                "audit_fraction": round(acc["audit_points"] / max(1, acc["fwd_points"]), 4),
+                "audit_violations": acc["lite_audit_violations"],
+                "redo_objects": acc["lite_redo_objects"],
+                "max_observed_lite_error": acc["lite_max_err"], "min_margin": acc["lite_min_margin"]},
+            "jac_points": {"surface": acc.get("jac_surface_points"), "render": acc.get("jac_render_points"),
+                           "render_backward_only": bool(acc.get("keep_masks"))},
+            "good_fraction": n_good / float(n_job * args.steps),
+            # inputs handed over in host memory: the upload added to one step
+            "host_inclusive_value": n_job / (elapsed / args.steps + create_s),
+            "batch_create_ms": create_s * 1e3,
             "cpu_baseline": None,
         }
-        tr = pmc_traffic(kernel)
+        tr = pmc_traffic(dom)
         if tr is not None:
             out["roofline"]["traffic"] = tr[0]
             out["roofline"]["traffic_source"] = tr[1]
+    shard.close()
+    if world == 1 and not args.no_extra:
+        # exact-decode leg: DSR_LITE=0 (every in-ball sample decoded in 3xFP16), same job
+        os.environ["DSR_LITE"] = "0"
+        ex = ResidentShard(opt, objs)
+        ex.run()
+        torch.cuda.synchronize()
+        k = min(args.steps, 3)
+        t1 = time.perf_counter()
+        for _ in range(k):
+            ex.run()
+        dt = time.perf_counter() - t1
+        ex.close()
+        del os.environ["DSR_LITE"]
+        out["value_exact"] = n_job * k / dt
+        out["value_exact_note"] = "DSR_LITE=0: no classification pass, every in-ball sample decoded exactly"
+        out["keyframe"] = keyframe_leg(dec)
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(n_pts=args.pts)
         print(json.dumps(out), flush=True)
-    lib.dsr_batch_destroy(batch)
     if dist is not None:
         dist.destroy_process_group()
 

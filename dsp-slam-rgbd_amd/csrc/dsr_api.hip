@@ -10,6 +10,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dsr.h"
@@ -90,7 +91,8 @@ static JacKernel jac_kernel() {
 // staggered wave groups (216: k_mlp_fwd_lite_st, bitwise equal to 88), +256 unscaled lite
 // weights with the bias in the accumulator and a packed fp16 ReLU epilogue (472), +1024
 // swizzled H image (1496, default: 2-way instead of 4-way epilogue store conflicts,
-// bitwise equal to 472); 18 and 984 are timing experiments (invalid results)
+// bitwise equal to 472).  18 and 984 are timing experiments whose results are invalid:
+// they exist only in a -DDSR_LITE_EXPERIMENTS build, never in the shipped library
 using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                             const float*, float*, ErtArgs);
 #ifndef DSR_DEFAULT_LITE_VARIANT
@@ -99,7 +101,10 @@ using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*,
 static LiteKernel lite_kernel() {
   const char* e = getenv("DSR_LITE_VARIANT");
   switch (e ? atoi(e) : DSR_DEFAULT_LITE_VARIANT) {
+#ifdef DSR_LITE_EXPERIMENTS
     case 18: return k_mlp_fwd_lite<true, 18>;
+    case 984: return k_mlp_fwd_lite_st<true, 88 + 256 + 512>;
+#endif
     case 16: return k_mlp_fwd_lite<true, 16>;
     case 32: return k_mlp_fwd_lite<true, 32>;
     case 40: return k_mlp_fwd_lite<true, 40>;
@@ -108,7 +113,6 @@ static LiteKernel lite_kernel() {
     case 24: return k_mlp_fwd_lite<true, 24>;
     case 88: return k_mlp_fwd_lite<true, 88>;
     case 216: return k_mlp_fwd_lite_st<true, 88>;
-    case 984: return k_mlp_fwd_lite_st<true, 88 + 256 + 512>;
     case 472: return k_mlp_fwd_lite_st<true, 88 + 256>;
   }
   return k_mlp_fwd_lite_st<true, 88 + 256 + 1024>;
@@ -178,6 +182,7 @@ struct dsr_batch {
   };
   std::vector<Group> groups;
   hipEvent_t fork_ev = nullptr;
+  hipEvent_t done_ev = nullptr;  // recorded after every run (dsr_batch_query)
   std::vector<hipEvent_t> join_ev;
   float* slots = nullptr;
   int* counts = nullptr;
@@ -190,6 +195,7 @@ struct dsr_batch {
   MaskArgs ma{nullptr, nullptr, nullptr, nullptr};   // kept masks of the exact re-decode
   int* kslot = nullptr;
   bool lite = true;             // lite classification pass + exact re-decode of the band
+  int loop_iters = 0;           // iters + 1 spare iteration for audit redos (lite + audit)
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
@@ -526,6 +532,23 @@ static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
   return 0;
 }
 
+// Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
+// (1.5): out-of-band samples with |y| < th + shell*margin are audited; DSR_LITE_AUDIT_LOG2
+// (7): plus a hashed 2^-log2 share of all other decoded samples; DSR_LITE_PERTURB: test hook
+static void lite_audit_args(ErtArgs& E) {
+  auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
+  const char* a = getenv("DSR_LITE_AUDIT");
+  E.audit = (a && atoi(a) == 0) ? 0 : 1;
+  E.shell = envf("DSR_LITE_SHELL", 1.5f);
+  E.audit_log2 = std::max(0, std::min(24, (int)envf("DSR_LITE_AUDIT_LOG2", 7.0f)));
+  E.perturb = envf("DSR_LITE_PERTURB", 0.0f);
+}
+static bool lite_audit_on() {
+  ErtArgs E{};
+  lite_audit_args(E);
+  return E.audit != 0;
+}
+
 static GNParams make_params(const dsr_optim_params* p) {
   GNParams P;
   P.k1 = p->k1; P.k2 = p->k2; P.k3 = p->k3; P.k4 = p->k4;
@@ -546,6 +569,7 @@ int dsr_batch_destroy(dsr_batch* b) {
   if (b->graph) hipGraphExecDestroy(b->graph);
   for (auto& e : b->join_ev) hipEventDestroy(e);
   if (b->fork_ev) hipEventDestroy(b->fork_ev);
+  if (b->done_ev) hipEventDestroy(b->done_ev);
   for (void* p : b->allocs) hipFree(p);
   delete b;
   return 0;
@@ -667,7 +691,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ALLOC(gr.sync, 8 * 32 * sizeof(unsigned));
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
-  ALLOC(b->counts, sizeof(int) * 4 * (size_t)std::max(1, b->iters) * n_obj);
+  b->loop_iters = b->iters + ((b->lite && lite_audit_on() && b->iters > 0) ? 1 : 0);
+  ALLOC(b->counts, sizeof(int) * NCOUNT * (size_t)std::max(1, b->loop_iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
   if (trace) {
     const size_t it = std::max(1, b->iters);
@@ -695,7 +720,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
   }
   b->passes = render_passes(M, (long)cand_off);
-  b->ev.resize((size_t)std::max(1, b->iters) * b->groups.size() * ev_per_iter(b) + 2);
+  b->ev.resize((size_t)std::max(1, b->loop_iters) * b->groups.size() * ev_per_iter(b) + 2);
   b->join_ev.resize(b->groups.size());
   for (auto& e : b->ev)
     if (hipEventCreate(&e) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
@@ -704,6 +729,10 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
       dsr_batch_destroy(b);
       return fail(ctx, "hipEventCreate failed");
     }
+  if (hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming) != hipSuccess) {
+    dsr_batch_destroy(b);
+    return fail(ctx, "hipEventCreate failed");
+  }
   if (hipEventCreateWithFlags(&b->fork_ev, hipEventDisableTiming) != hipSuccess) {
     dsr_batch_destroy(b);
     return fail(ctx, "hipEventCreate failed");
@@ -766,10 +795,8 @@ int dsr_batch_graph(dsr_batch* b) {
   return batch_capture(b);
 }
 
-int dsr_batch_run(dsr_batch* b) {
-  if (!b) return -2;
+static int batch_launch(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
-  hipSetDevice(ctx->device);
   if (!graph_enabled() || b->runs++ == 0) return batch_enqueue(b);
   if (!b->graph || b->graph_key != graph_key()) {
     const int rc = batch_capture(b);
@@ -781,6 +808,26 @@ int dsr_batch_run(dsr_batch* b) {
   b->ran = true;
   b->timed = false;
   return 0;
+}
+
+int dsr_batch_run(dsr_batch* b) {
+  if (!b) return -2;
+  dsr_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  const int rc = batch_launch(b);
+  if (rc) return rc;
+  DSR_CHECK(ctx, hipEventRecord(b->done_ev, ctx->stream));
+  return 0;
+}
+
+int dsr_batch_query(dsr_batch* b) {
+  if (!b) return -2;
+  if (!b->ran) return fail(b->ctx, "batch has not run");
+  hipSetDevice(b->ctx->device);
+  const hipError_t e = hipEventQuery(b->done_ev);
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return fail(b->ctx, std::string("hipEventQuery: ") + hipGetErrorString(e));
 }
 
 static int batch_enqueue(dsr_batch* b, bool timing) {
@@ -799,10 +846,13 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
   if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
-  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s0, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf);
+  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s0, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf,
+                     b->iters);
   DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
   for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
-  for (int it = 0; it < b->iters; ++it) {
+  // the last of loop_iters (lite + audit) is spare: only objects whose iteration an audit
+  // discarded (k_solve) are still running there, every other object's kernels return at once
+  for (int it = 0; it < b->loop_iters; ++it) {
     for (int g = 0; g < G; ++g) {             // groups interleaved, one stream each
       const dsr_batch::Group& gr = b->groups[g];
       hipStream_t s = ctx->gstream[g];
@@ -814,7 +864,8 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
       float* b4 = b->bias4f + (size_t)o0 * HID;
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
-      const ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
+      ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
+      lite_audit_args(ert);
       DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
                                        (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
@@ -860,7 +911,7 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
                          keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
       hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
-                         b->counts + (size_t)o0 * 4, n);
+                         b->counts + (size_t)o0 * NCOUNT, n);
       hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, b->slots,
                          b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
                          b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
@@ -905,7 +956,13 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
-  for (int it = 0; it < (b->timed ? b->iters : 0); ++it)
+  std::vector<ObjState> hs(b->n_obj);
+  DSR_CHECK(b->ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
+  // the spare iteration (audit redo) counts only when some object ran in it
+  bool spare_used = false;
+  for (const ObjState& o : hs) spare_used = spare_used || o.lite_redo;
+  const int used_iters = (b->loop_iters > b->iters && !spare_used) ? b->iters : b->loop_iters;
+  for (int it = 0; it < (b->timed ? used_iters : 0); ++it)
     for (int g = 0; g < G; ++g) {
       const hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       for (int pz = 0; pz < np; ++pz) {
@@ -922,29 +979,81 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
     }
   DSR_CHECK(b->ctx, hipEventElapsedTime(&ms, b->ev[0], b->ev[1]));
   st->total_ms = ms;
-  st->fwd_launches = b->timed ? b->iters * np * G : 0;
-  st->jac_launches = b->timed ? b->iters * G : 0;
-  st->refine_launches = (b->timed && b->lite) ? b->iters * G : 0;
+  st->fwd_launches = b->timed ? used_iters * np * G : 0;
+  st->jac_launches = b->timed ? used_iters * G : 0;
+  st->refine_launches = (b->timed && b->lite) ? used_iters * G : 0;
   st->lite = b->lite ? 1 : 0;
+  st->keep_masks = (b->lite && b->ma.msk && fwd_variant() == 12) ? 1 : 0;
   if (b->lite) {
-    std::vector<ObjState> hs(b->n_obj);
-    DSR_CHECK(b->ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
     st->lite_min_margin = 1e30;
     for (const ObjState& o : hs) {
       st->lite_max_err = std::max(st->lite_max_err, (double)o.lite_err);
       if (o.iters_done > 0) st->lite_min_margin = std::min(st->lite_min_margin, (double)o.lite_margin);
+      st->lite_audit_violations += o.lite_viol_total;
+      st->lite_redo_objects += o.lite_redo ? 1 : 0;
     }
   }
-  std::vector<int> c((size_t)4 * std::max(1, b->iters) * b->n_obj);
+  std::vector<int> c((size_t)NCOUNT * std::max(1, b->loop_iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
-  for (int it = 0; it < b->iters; ++it)
+  for (int it = 0; it < b->loop_iters; ++it)
     for (int o = 0; o < b->n_obj; ++o) {
-      const int* e = c.data() + ((size_t)it * b->n_obj + o) * 4;
+      const int* e = c.data() + ((size_t)it * b->n_obj + o) * NCOUNT;
       st->fwd_points += e[0];
       st->jac_points += e[1];
       st->inball_points += e[2];
       st->refine_points += e[3];
+      st->audit_points += e[4];
+      st->jac_render_points += e[5];
+      st->jac_surface_points += e[1] - e[5];
     }
+  return 0;
+}
+
+// Multi-GPU from one process: longest-processing-time-first partition of
+// the objects over the devices (cost = n_rays * M + n_pts, the decoder work of one
+// iteration, greedy to the least loaded device; the same rule as reconstruct/parallel.py),
+// one host thread per device running its shard through dsr_reconstruct_batch, every
+// out-record written back in input order — host memory is the gather point, so no
+// collective is needed inside one process.  Objects never interact: each result is
+// bitwise the one a single-device batch gives.
+int dsr_reconstruct_multi(dsr_ctx* const* ctxs, const dsr_decoder* const* decs, int n_dev,
+                          const dsr_optim_params* p, int n_obj, const dsr_object_in* in, dsr_object_out* out) {
+  if (!ctxs || !decs || n_dev <= 0 || !ctxs[0]) return -2;
+  dsr_ctx* c0 = ctxs[0];
+  if (!p || !out || (n_obj > 0 && !in)) return fail(c0, "null argument");
+  if (n_obj <= 0) return fail(c0, "n_obj must be > 0");
+  for (int g = 0; g < n_dev; ++g)
+    if (!ctxs[g] || !decs[g]) return fail(c0, "null context or decoder");
+  std::vector<int> order(n_obj);
+  for (int i = 0; i < n_obj; ++i) order[i] = i;
+  auto cost = [&](int i) { return (double)in[i].n_rays * p->num_depth_samples + in[i].n_pts; };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
+  std::vector<double> load(n_dev, 0.0);
+  std::vector<std::vector<int>> shard(n_dev);
+  for (int i : order) {
+    const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    shard[g].push_back(i);
+    load[g] += cost(i);
+  }
+  std::vector<int> rc(n_dev, 0);
+  std::vector<std::vector<dsr_object_out>> res(n_dev);
+  auto run = [&](int g) {
+    std::vector<int>& sh = shard[g];
+    if (sh.empty()) return;
+    std::sort(sh.begin(), sh.end());
+    std::vector<dsr_object_in> sin;
+    for (int i : sh) sin.push_back(in[i]);
+    res[g].resize(sh.size());
+    rc[g] = dsr_reconstruct_batch(ctxs[g], decs[g], p, (int)sh.size(), sin.data(), res[g].data(), nullptr);
+  };
+  std::vector<std::thread> th;
+  for (int g = 1; g < n_dev; ++g) th.emplace_back(run, g);
+  run(0);
+  for (auto& t : th) t.join();
+  for (int g = 0; g < n_dev; ++g)
+    if (rc[g]) return fail(c0, "device shard " + std::to_string(g) + ": " + ctxs[g]->err);
+  for (int g = 0; g < n_dev; ++g)
+    for (size_t k = 0; k < shard[g].size(); ++k) out[shard[g][k]] = res[g][k];
   return 0;
 }
 
@@ -1198,105 +1307,154 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   return 0;
 }
 
-int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, const float* t_co_se3,
-                  float scale, const float* pts, int n_pts, const float* code, float* t_out) {
-  // Optimizer.estimate_pose_cam_obj (optimizer.py:46-87)
-  if (!ctx || !dec || !p || !t_co_se3 || !code || !t_out || (n_pts > 0 && !pts)) return fail(ctx, "null argument");
-  if (n_pts <= 0) return fail(ctx, "pose-only GN needs surface points");
+// Optimizer.estimate_pose_cam_obj (optimizer.py:46-87) for n_obj independent objects in
+// one device pass per GN iteration: one fwd+Jacobian launch over every object's tiles (the
+// Jacobian kernel's tiles carry their object), one k_solve_pose workgroup per object.  The
+// reference's iteration-4 inlier filter (:77-79, only effective past 5 iterations) is a
+// host compaction of each object's points.
+int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int n_obj,
+                        const dsr_pose_in* in, float* t_out) {
+  if (!ctx || !dec || !p || !t_out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
+  if (n_obj <= 0) return fail(ctx, "n_obj must be > 0");
+  if (p->code_len != dec->code_len) return fail(ctx, "optimizer code_len != decoder code_len");
+  for (int o = 0; o < n_obj; ++o) {
+    if (!in[o].code || (in[o].n_pts > 0 && !in[o].pts)) return fail(ctx, "null argument");
+    if (in[o].n_pts <= 0) return fail(ctx, "pose-only GN needs surface points");
+  }
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
-  float t_in[16];
-  for (int i = 0; i < 16; ++i) t_in[i] = t_co_se3[i];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) t_in[i * 4 + j] = t_in[i * 4 + j] * scale;     // :56 (fp32)
-  std::vector<float> hp(pts, pts + (size_t)n_pts * 3);
-  int n = n_pts;
+  std::vector<float> t_in((size_t)16 * n_obj), hz((size_t)CODE * n_obj);
+  std::vector<std::vector<float>> hp(n_obj);
+  size_t cap_pts = 0, cap_tiles = 0;
+  for (int o = 0; o < n_obj; ++o) {
+    const dsr_pose_in& x = in[o];
+    for (int i = 0; i < 16; ++i) t_in[16 * o + i] = x.t_co_se3[i];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) t_in[16 * o + i * 4 + j] = t_in[16 * o + i * 4 + j] * x.scale;   // :56 (fp32)
+    std::copy(x.code, x.code + CODE, hz.begin() + (size_t)CODE * o);
+    hp[o].assign(x.pts, x.pts + (size_t)x.n_pts * 3);
+    cap_pts += x.n_pts;
+    cap_tiles += (x.n_pts + TILE - 1) / TILE;
+  }
   const int iters = p->pose_only_iterations;
-  const int cap_tiles = (n + TILE - 1) / TILE;
   void *dpts = nullptr, *dst = nullptr, *dz = nullptr, *db0 = nullptr, *db4 = nullptr, *dt = nullptr,
        *dnt = nullptr, *dslots = nullptr, *ddesc = nullptr, *dtin = nullptr, *doc = nullptr, *dzb = nullptr,
        *dres = nullptr, *dout = nullptr;
   std::vector<void*> al;
   auto A = [&](void** q, size_t bytes) {
-    if (hipMalloc(q, bytes) != hipSuccess) return false;
+    if (hipMalloc(q, std::max<size_t>(bytes, 256)) != hipSuccess) return false;
     al.push_back(*q);
     return true;
   };
   auto cleanup = [&]() { for (void* q : al) hipFree(q); };
-  if (!A(&dpts, sizeof(float) * 3 * n) || !A(&dst, sizeof(ObjState)) || !A(&dz, sizeof(float) * CODE) ||
-      !A(&db0, sizeof(float) * HID) || !A(&db4, sizeof(float) * HID) || !A(&dt, sizeof(Tile) * cap_tiles) ||
-      !A(&dnt, sizeof(int)) || !A(&dslots, sizeof(float) * SLOT_FLOATS * cap_tiles) ||
-      !A(&ddesc, sizeof(ObjDesc)) || !A(&dtin, sizeof(float) * 16) || !A(&doc, sizeof(int)) ||
-      !A(&dzb, sizeof(float) * CODE) || !A(&dres, sizeof(float) * n) || !A(&dout, sizeof(float) * 16)) {
+  const size_t n = (size_t)n_obj;
+  if (!A(&dpts, sizeof(float) * 3 * cap_pts) || !A(&dst, sizeof(ObjState) * n) ||
+      !A(&dz, sizeof(float) * CODE * n) || !A(&db0, sizeof(float) * HID * n) || !A(&db4, sizeof(float) * HID * n) ||
+      !A(&dt, sizeof(Tile) * cap_tiles) || !A(&dnt, sizeof(int)) ||
+      !A(&dslots, sizeof(float) * SLOT_FLOATS * cap_tiles) || !A(&ddesc, sizeof(ObjDesc) * n) ||
+      !A(&dtin, sizeof(float) * 16 * n) || !A(&doc, sizeof(int) * n) || !A(&dzb, sizeof(float) * CODE * n) ||
+      !A(&dres, sizeof(float) * cap_pts) || !A(&dout, sizeof(float) * 16 * n)) {
     cleanup();
     return fail(ctx, "hipMalloc failed (pose_only)");
   }
-  const int zero = 0;
-  bool ok = hipMemcpy(dpts, hp.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(dz, code, sizeof(float) * CODE, hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(dtin, t_in, sizeof(float) * 16, hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(doc, &zero, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+  const std::vector<int> zeros(n, 0);
+  bool ok = hipMemcpy(dz, hz.data(), sizeof(float) * CODE * n, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dtin, t_in.data(), sizeof(float) * 16 * n, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(doc, zeros.data(), sizeof(int) * n, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only)"); }
   const DevDecoder& D = dec->D;
   GNParams P = make_params(p);
   P.raw_residual = 1;
-  hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)dz, (float*)db0, (float*)db4);
-  hipLaunchKernelGGL(k_init_state, dim3(1), dim3(64), 0, s, 1, (const float*)dtin, (const int*)doc,
-                     (const float*)dz, (ObjState*)dst, (float*)dzb);                  // :57 t_obj_cam = inv
-  auto upload_tiles = [&](int npts) {
-    ObjDesc d{};
-    d.n_pts = npts;
-    const int nt = (npts + TILE - 1) / TILE;
-    std::vector<Tile> ht(nt);
-    for (int t = 0; t < nt; ++t) ht[t] = Tile{0, 0, t * TILE, std::min(TILE, npts - t * TILE)};
-    return hipMemcpy(ddesc, &d, sizeof(ObjDesc), hipMemcpyHostToDevice) == hipSuccess &&
-           (nt == 0 || hipMemcpy(dt, ht.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice) == hipSuccess) &&
-           hipMemcpy(dnt, &nt, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+  for (int o = 0; o < n_obj; ++o)
+    hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)dz + (size_t)CODE * o,
+                       (float*)db0 + (size_t)HID * o, (float*)db4 + (size_t)HID * o);
+  hipLaunchKernelGGL(k_init_state, dim3(n_obj), dim3(64), 0, s, n_obj, (const float*)dtin, (const int*)doc,
+                     (const float*)dz, (ObjState*)dst, (float*)dzb, 1);               // :57 t_obj_cam = inv
+  int n_tiles = 0;
+  // points, descriptors and tile table of the current point sets (objects back to back)
+  auto upload = [&]() {
+    std::vector<ObjDesc> hd(n);
+    std::vector<Tile> ht;
+    std::vector<float> all;
+    int poff = 0, soff = 0;
+    for (int o = 0; o < n_obj; ++o) {
+      const int np = (int)(hp[o].size() / 3);
+      hd[o].pts_off = poff;
+      hd[o].n_pts = np;
+      hd[o].slot_sdf = soff;
+      for (int t = 0; t * TILE < np; ++t) ht.push_back(Tile{o, 0, t * TILE, std::min(TILE, np - t * TILE)});
+      all.insert(all.end(), hp[o].begin(), hp[o].end());
+      poff += np;
+      soff += (np + TILE - 1) / TILE;
+    }
+    n_tiles = (int)ht.size();
+    return (all.empty() || hipMemcpy(dpts, all.data(), sizeof(float) * all.size(), hipMemcpyHostToDevice) == hipSuccess) &&
+           hipMemcpy(ddesc, hd.data(), sizeof(ObjDesc) * n, hipMemcpyHostToDevice) == hipSuccess &&
+           (ht.empty() || hipMemcpy(dt, ht.data(), sizeof(Tile) * ht.size(), hipMemcpyHostToDevice) == hipSuccess) &&
+           hipMemcpy(dnt, &n_tiles, sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!upload_tiles(n)) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only tiles)"); }
+  if (!upload()) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only tiles)"); }
+  std::vector<char> emptied(n, 0);
   for (int e = 0; e < iters; ++e) {
-    const int nt = (n + TILE - 1) / TILE;
     const bool filter = (e == 4) && (e + 1 < iters);   // :77-79 inlier filter (effective only past 5 iters)
-    hipLaunchKernelGGL(jac_kernel(), dim3(std::max(1, std::min(ctx->n_cu, nt))), dim3(512), 0, s, D, (const Tile*)dt,
-                       (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst, (const float*)dpts,
-                       (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
-                       (float*)dslots, (const float4*)nullptr, (float*)nullptr, filter ? (float*)dres : (float*)nullptr,
-                       MaskArgs{nullptr, nullptr, nullptr, nullptr});
-    hipLaunchKernelGGL(k_solve_pose, dim3(1), dim3(256), 0, s, nt, n, (ObjState*)dst, (const float*)dslots);
+    if (n_tiles > 0)
+      hipLaunchKernelGGL(jac_kernel(), dim3(std::max(1, std::min(ctx->n_cu, n_tiles))), dim3(512), 0, s, D,
+                         (const Tile*)dt, (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst,
+                         (const float*)dpts, (const float4*)nullptr, (const float*)nullptr, (const float*)db0,
+                         (const float*)db4, P, (float*)dslots, (const float4*)nullptr, (float*)nullptr,
+                         filter ? (float*)dres : (float*)nullptr, MaskArgs{nullptr, nullptr, nullptr, nullptr});
+    hipLaunchKernelGGL(k_solve_pose, dim3(n_obj), dim3(256), 0, s, (const ObjDesc*)ddesc, (ObjState*)dst,
+                       (const float*)dslots);
     if (filter) {
-      std::vector<float> res(n);
+      size_t tot = 0;
+      for (int o = 0; o < n_obj; ++o) tot += hp[o].size() / 3;
+      std::vector<float> res(std::max<size_t>(1, tot));
       if (hipStreamSynchronize(s) != hipSuccess ||      // ctx->stream is non-blocking
-          hipMemcpy(res.data(), dres, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess) {
+          (tot && hipMemcpy(res.data(), dres, sizeof(float) * tot, hipMemcpyDeviceToHost) != hipSuccess)) {
         cleanup();
         return fail(ctx, "hipMemcpy failed (pose_only residuals)");
       }
-      std::vector<float> kept;
-      for (int i = 0; i < n; ++i)
-        if (std::fabs(res[i]) <= 0.05f) kept.insert(kept.end(), hp.begin() + 3 * i, hp.begin() + 3 * i + 3);
-      hp.swap(kept);
-      n = (int)(hp.size() / 3);
-      if (n == 0) {
-        // the reference goes on with an empty point set: J^T J / 0 -> NaN pose
-        for (int i = 0; i < 16; ++i) t_out[i] = __builtin_nanf("");
-        cleanup();
-        return 0;
+      size_t off = 0;
+      for (int o = 0; o < n_obj; ++o) {
+        const size_t np = hp[o].size() / 3;
+        std::vector<float> kept;
+        for (size_t i = 0; i < np; ++i)
+          if (std::fabs(res[off + i]) <= 0.05f) kept.insert(kept.end(), hp[o].begin() + 3 * i, hp[o].begin() + 3 * i + 3);
+        off += np;
+        hp[o].swap(kept);
+        if (hp[o].empty()) emptied[o] = 1;    // the reference goes on with an empty set: NaN pose
       }
-      if (hipMemcpy(dpts, hp.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice) != hipSuccess || !upload_tiles(n)) {
-        cleanup();
-        return fail(ctx, "hipMemcpy failed (pose_only filter)");
-      }
+      if (!upload()) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only filter)"); }
     }
   }
-  hipLaunchKernelGGL(k_inv_out, dim3(1), dim3(64), 0, s, (const ObjState*)dst, (float*)dout);   // :84
-  float T[16];
+  hipLaunchKernelGGL(k_inv_out, dim3((n_obj + 63) / 64), dim3(64), 0, s, n_obj, (const ObjState*)dst,
+                     (float*)dout);                                                    // :84
+  std::vector<float> T((size_t)16 * n);
   ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
-       hipMemcpy(T, dout, sizeof(float) * 16, hipMemcpyDeviceToHost) == hipSuccess;
+       hipMemcpy(T.data(), dout, sizeof(float) * 16 * n, hipMemcpyDeviceToHost) == hipSuccess;
   cleanup();
   if (!ok) return fail(ctx, "pose_only failed");
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) T[i * 4 + j] = T[i * 4 + j] / scale;                 // :85
-  for (int i = 0; i < 16; ++i) t_out[i] = T[i];
+  for (int o = 0; o < n_obj; ++o) {
+    float* to = t_out + 16 * o;
+    for (int i = 0; i < 16; ++i) to[i] = T[16 * o + i];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) to[i * 4 + j] = to[i * 4 + j] / in[o].scale;           // :85
+    if (emptied[o])                     // J^T J / 0 in the reference: the pose turns NaN
+      for (int i = 0; i < 16; ++i) to[i] = __builtin_nanf("");
+  }
   return 0;
+}
+
+int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, const float* t_co_se3,
+                  float scale, const float* pts, int n_pts, const float* code, float* t_out) {
+  if (!t_co_se3) return fail(ctx, "null argument");
+  dsr_pose_in x;
+  for (int i = 0; i < 16; ++i) x.t_co_se3[i] = t_co_se3[i];
+  x.scale = scale;
+  x.pts = pts;
+  x.n_pts = n_pts;
+  x.code = code;
+  return dsr_pose_only_batch(ctx, dec, p, 1, &x, t_out);
 }
 
 }  // extern "C"

@@ -85,6 +85,10 @@ struct ObjState {
   int n_refine;          // of which re-decoded exactly after the lite pass
   float lite_margin;     // this iteration's classification margin (dsr_mlp_lite.hpp)
   float lite_err;        // max |lite - exact| seen on this object's re-decoded samples
+  int n_audit;           // this iteration's audited out-of-band samples (k_refine_compact)
+  int lite_viol;         // this iteration's audited samples whose exact class differs
+  int lite_viol_total;   // over the run
+  int lite_redo;         // 1: an iteration was discarded for a violation; exact from then on
 };
 
 struct Tile {
@@ -101,7 +105,39 @@ struct ErtArgs {
   ObjState* st;          // lite pass: per-object margin; exact re-decode: per-object error
   unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
   int lag;               // staggered lite pass: k step at which group B may start a GEMM
+  // lite-pass audit (dsr_mlp_lite.hpp: lite_flag): out-of-band samples with |y| < th +
+  // shell*margin, and a hashed 2^-audit_log2 share of all others, are re-decoded exactly too
+  int audit;             // 0: no audit
+  float shell;
+  int audit_log2;
+  float perturb;         // test hook (DSR_LITE_PERTURB): lite values moved by +-perturb
 };
+
+// bit 30 of a refine candidate's sample index (cand[].w): the sample is an audit, not a band sample
+constexpr int AUDIT_BIT = 1 << 30;
+
+// Lite-pass classification of one decoded sample (lite value y, index idx = ray*M + j)
+// into the refine flags k_refine_compact consumes: 1 = band (|y| < th + margin, NaN, or
+// the range guard), 2 = audited certainly-empty sample, 3 = audited certainly-full sample
+// (3 also terminates the ray, like an unaudited full sample).  Returns the flag (0: none)
+// and sets `full` when the sample is certainly full.
+__device__ __forceinline__ unsigned char lite_flag(const ErtArgs& E, float y, int idx, float margin,
+                                                   int salt, bool& full) {
+  full = false;
+  if (!(y >= -E.nth + margin) && !(y <= E.nth - margin)) return 1;      // band (or NaN)
+  full = y <= E.nth - margin;
+  if (!E.audit) return 0;
+  const unsigned h = (unsigned)(idx ^ (salt * 0x5bd1e995)) * 2654435761u;
+  const bool au = fabsf(y) < -E.nth + E.shell * margin ||
+                  (E.audit_log2 > 0 && (h >> (32 - E.audit_log2)) == 0u);
+  return au ? (full ? 3 : 2) : 0;
+}
+
+// test hook: a deterministic +-perturb on every lite value (DSR_LITE_PERTURB)
+__device__ __forceinline__ float lite_perturb(const ErtArgs& E, float y, int idx) {
+  if (E.perturb == 0.f) return y;
+  return y + ((((unsigned)idx * 2654435761u) >> 31) ? E.perturb : -E.perturb);
+}
 
 // ReLU masks + SDF of the samples the exact pass re-decodes after the lite pass, so the
 // Jacobian kernel runs only the backward chain for render points (loss.py:157 re-forwards

@@ -174,7 +174,7 @@ __device__ __forceinline__ float3 xform(const float* T, float x, float y, float 
 // state init / per-iteration prologue
 // ------------------------------------------------------------------------------------
 __global__ void k_init_state(int n_obj, const float* __restrict__ t_in, const int* __restrict__ is_oc,
-                             const float* __restrict__ z_in, ObjState* st, float* zbuf) {
+                             const float* __restrict__ z_in, ObjState* st, float* zbuf, int iters) {
   const int o = blockIdx.x;
   if (o >= n_obj) return;
   if (threadIdx.x < CODE) zbuf[o * CODE + threadIdx.x] = z_in[o * CODE + threadIdx.x];
@@ -186,12 +186,15 @@ __global__ void k_init_state(int n_obj, const float* __restrict__ t_in, const in
       inv_small<4>(t_in + o * 16, S.T);      // optimizer.py:105-106
     }
     S.loss = 0.f;                              // optimizer.py:119
-    S.status = ST_RUNNING;
+    // zero iterations: the loop body never runs and the reference returns the input pose
+    // and code with is_good=True, loss 0. (optimizer.py:120, 201-205)
+    S.status = iters > 0 ? ST_RUNNING : ST_DONE;
     S.fail_reason = 0;
     S.iters_done = 0;
     S.n_valid = S.k = 0;
     S.sdf_loss = S.render_loss = 0.f;
     S.lite_margin = S.lite_err = 0.f;
+    S.n_audit = S.lite_viol = S.lite_viol_total = S.lite_redo = 0;
   }
 }
 
@@ -234,7 +237,10 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
     S.n_valid = 0;
     S.k = 0;
     S.n_emit = S.n_eval = S.n_refine = 0;
-    if (S.iters_done == 0) {
+    S.n_audit = S.lite_viol = 0;
+    if (S.lite_redo) {                                  // an audit caught a misclassification:
+      S.lite_margin = 1e30f;                            // every sample exact from now on
+    } else if (S.iters_done == 0) {
       S.lite_margin = P.lite_margin0;
     } else {
       const float m = fmaxf(P.lite_floor, P.lite_safety * S.lite_err);
@@ -428,13 +434,16 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) base_s = 0;
   __syncthreads();
-  __shared__ uint64_t rbits[SAMPLE_THREADS];
+  __shared__ uint64_t rbits[SAMPLE_THREADS], abits[SAMPLE_THREADS];
   const float full = nth - S.lite_margin;
+  int n_audit = 0;
   for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
     const int ray = r0 + tid;
     // Each wave scans 64 rays one at a time, lane j on sample j (coalesced flag / value
     // loads, ballots): refined = the flagged samples in front of the first unflagged sample
-    // that is certainly full; every flag is cleared.
+    // that is certainly full, or up to and including it when it is an audited full sample
+    // (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag) ride along in bit 30 of
+    // the candidate's index so the exact pass can check their class.
     for (int i0 = 0; i0 < 64; i0 += 8) {     // 8 rays' loads in flight
       unsigned char fv[8];
       float yv[8];
@@ -449,14 +458,24 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int rr = r0 + 64 * wv + i0 + u;
-        const uint64_t fb = __ballot(fv[u] != 0), ub = __ballot(fv[u] == 0 && yv[u] <= full);
-        const uint64_t b = ub ? (fb & ((1ull << __builtin_ctzll(ub)) - 1)) : fb;
+        const uint64_t fb = __ballot(fv[u] != 0);
+        const uint64_t ub = __ballot((fv[u] == 0 || fv[u] == 3) && yv[u] <= full);
+        const uint64_t tb = __ballot(fv[u] == 3), ab = __ballot(fv[u] >= 2);
+        uint64_t b = fb;
+        if (ub) {
+          const int stop = __builtin_ctzll(ub);
+          b = fb & (((1ull << stop) - 1) | (tb & (1ull << stop)));
+        }
         if (rr < d.n_rays && lane < M) refine[d.cand_off + (size_t)rr * M + lane] = 0;
-        if (lane == i0 + u) rbits[tid] = b;
+        if (lane == i0 + u) {
+          rbits[tid] = b;
+          abits[tid] = b & ab;
+        }
       }
     }
-    const uint64_t bits = rbits[tid];
+    const uint64_t bits = rbits[tid], aud = abits[tid];
     const int cnt = __popcll(bits);
+    n_audit += __popcll(aud);
     const int inc = wave_incl_scan(cnt, lane);
     if (lane == 63) wsum[wv] = inc;
     __syncthreads();
@@ -466,7 +485,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
       const int j = __builtin_ctzll(m);
       const float3 x = ray_sample(rays, S, ray, j);
       if (slotmap) slotmap[d.cand_off + ray * M + j] = off;
-      cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
+      const int tag = ((aud >> j) & 1) ? AUDIT_BIT : 0;
+      cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float((ray * M + j) | tag));
     }
     __syncthreads();
     if (tid == 0) {
@@ -476,6 +496,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, co
     }
     __syncthreads();
   }
+  if (n_audit) atomicAdd(&S.n_audit, n_audit);
   if (tid == 0) {
     S.n_emit = base_s;
     S.n_refine = base_s;
@@ -626,7 +647,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
       float s = sm.red[tid];
       for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
       const float y = tanhf(s + D.b8);
-      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]);
+      const int idx = __float_as_int(sm.xyz[tid * 4 + 3]) & ~AUDIT_BIT;   // (audit tag: lite_flag)
       dense[d.cand_off + idx] = y;
       if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;
     }
@@ -1291,8 +1312,19 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
-  const ObjDesc d = desc[o];
   const int tid = threadIdx.x;
+  if (S.lite_viol > 0) {
+    // An audited sample's exact class differs from the lite pass's (dsr_mlp16.hpp): some
+    // unaudited sample may be misclassified too, so this iteration's terms are not trusted.
+    // Discard it — no update, no trace, no failure exit — and redo it with every sample
+    // decoded exactly (k_iter_begin); dsr_batch_run enqueues one spare iteration for this.
+    if (tid == 0) {
+      S.lite_viol_total += S.lite_viol;
+      S.lite_redo = 1;
+    }
+    return;
+  }
+  const ObjDesc d = desc[o];
   __shared__ float Ss[SLOT_FLOATS];
   __shared__ float Sr[SLOT_FLOATS];
   __shared__ float A[NPAR][NPAR + 1];
@@ -1572,16 +1604,22 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
 // H = J^T J / N + 1e-2 I (6x6, se3 part of the Sim(3) J), b = -J^T r / N (raw residual),
 // dx = inverse(H) b, T <- exp_se3(dx) T.
 // ------------------------------------------------------------------------------------
-__global__ void k_solve_pose(int n_tiles, int n_pts, ObjState* st, const float* __restrict__ slots) {
+// One workgroup per object (dsr_pose_only_batch); objects with no points left are skipped.
+__global__ void k_solve_pose(const ObjDesc* __restrict__ desc, ObjState* st, const float* __restrict__ slots) {
+  const int o = blockIdx.x;
+  const ObjDesc d = desc[o];
+  if (d.n_pts <= 0) return;
+  const int n_tiles = (d.n_pts + TILE - 1) / TILE;
+  const float* sl = slots + (size_t)d.slot_sdf * SLOT_FLOATS;
   __shared__ float S[SLOT_FLOATS];
   for (int e = threadIdx.x; e < SLOT_FLOATS; e += blockDim.x) {
     double a = 0.0;
-    for (int t = 0; t < n_tiles; ++t) a += (double)slots[(size_t)t * SLOT_FLOATS + e];
+    for (int t = 0; t < n_tiles; ++t) a += (double)sl[(size_t)t * SLOT_FLOATS + e];
     S[e] = (float)a;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const float N = (float)n_pts;
+  const float N = (float)d.n_pts;
   float H[36], Hi[36], b[6], dx[6], dT[16], Tn[16];
   for (int a = 0; a < 6; ++a)
     for (int c = 0; c < 6; ++c) {
@@ -1597,25 +1635,35 @@ __global__ void k_solve_pose(int n_tiles, int n_pts, ObjState* st, const float* 
     dx[a] = s;
   }
   exp_se3_dev(dx, dT);
-  mm4(dT, st[0].T, Tn);
-  for (int i = 0; i < 16; ++i) st[0].T[i] = Tn[i];
+  mm4(dT, st[o].T, Tn);
+  for (int i = 0; i < 16; ++i) st[o].T[i] = Tn[i];
 }
 
-__global__ void k_inv_out(const ObjState* __restrict__ st, float* __restrict__ out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) inv_small<4>(st[0].T, out);
+__global__ void k_inv_out(int n_obj, const ObjState* __restrict__ st, float* __restrict__ out) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < n_obj) inv_small<4>(st[o].T, out + 16 * o);
 }
 
-// per-iteration counters for the algorithmic-FLOP bookkeeping
+// per-iteration counters for the algorithmic-FLOP bookkeeping:
+// decoded samples, Jacobian points (N + K), in-ball samples, exact re-decodes, audits, K
+constexpr int NCOUNT = 6;
 __global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
                         int it, int* __restrict__ counts, int stride) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= n_obj) return;
   const ObjState& S = st[o];
-  int* c = counts + ((size_t)it * stride + o) * 4;
+  int* c = counts + ((size_t)it * stride + o) * NCOUNT;
+  if (S.status != ST_RUNNING) {                 // finished / failed objects did no work
+    for (int i = 0; i < NCOUNT; ++i) c[i] = 0;
+    return;
+  }
+  const bool jac = S.n_ren_tiles > 0 || S.k > 0;
   c[0] = S.n_eval;
-  c[1] = (S.n_ren_tiles > 0 || S.k > 0) ? desc[o].n_pts + S.k : 0;
+  c[1] = jac ? desc[o].n_pts + S.k : 0;
   c[2] = S.n_valid;
   c[3] = S.n_refine;
+  c[4] = S.n_audit;
+  c[5] = jac ? S.k : 0;                         // render points of c[1] (the rest: surface)
 }
 
 __global__ void k_finalize(int n_obj, const ObjState* __restrict__ st, const float* __restrict__ zbuf,

@@ -505,10 +505,17 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
         const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
         if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) y = __builtin_nanf("");
-        const int idx = __float_as_int(p.w);
-        if (E.st) {                        // re-decode of a lite band sample: track the lite error
-          const float e = fabsf(y - dense[d.cand_off + idx]);
+        const int tagged = __float_as_int(p.w);
+        const int idx = tagged & ~AUDIT_BIT;
+        if (E.st) {                        // re-decode after the lite pass: track the lite error
+          const float yl = dense[d.cand_off + idx];
+          const float e = fabsf(y - yl);
           if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+          if (tagged & AUDIT_BIT) {        // audited out-of-band sample: same class exactly?
+            const int cl = yl <= E.nth ? 0 : (yl < -E.nth ? 1 : 2);   // full | band | empty
+            const int ce = y <= E.nth ? 0 : (y < -E.nth ? 1 : 2);
+            if (cl != ce) atomicAdd(&E.st[tl.obj].lite_viol, 1);
+          }
         }
         dense[d.cand_off + idx] = y;
         if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;

@@ -411,11 +411,14 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
         if (p.x != p.x || p.y != p.y || p.z != p.z || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
           y = __builtin_nanf("");
         const int idx = __float_as_int(p.w);
-        const float margin = E.st[tl.obj].lite_margin;
+        const ObjState& So = E.st[tl.obj];
+        const float margin = So.lite_margin;
+        y = lite_perturb(E, y, idx);
         dense[d.cand_off + idx] = y;
-        if ((LV & 8) && sm.ovf) E.refine[d.cand_off + idx] = 1;                   // range guard
-        else if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;            // certainly full
-        else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;          // band (or NaN)
+        bool full = false;
+        const unsigned char fl = ((LV & 8) && sm.ovf) ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
+        if (fl) E.refine[d.cand_off + idx] = fl;                 // band / range guard / audit
+        if (fl != 1 && full) E.dead[d.ray_off + idx / E.M] = 1;  // certainly full
       }
     }
     __syncthreads();
@@ -714,11 +717,15 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           if (pt.x != pt.x || pt.y != pt.y || pt.z != pt.z || bias0f[tl.obj * HID] != bias0f[tl.obj * HID])
             y = __builtin_nanf("");
           const int idx = __float_as_int(pt.w);
-          const float margin = E.st[tl.obj].lite_margin;
+          const ObjState& So = E.st[tl.obj];
+          const float margin = So.lite_margin;
+          y = lite_perturb(E, y, idx);
           dense[d.cand_off + idx] = y;
-          if (sm.ovf[p] == it + 1 || sm.broken) E.refine[d.cand_off + idx] = 1;     // range guard
-          else if (y <= E.nth - margin) E.dead[d.ray_off + idx / E.M] = 1;          // certainly full
-          else if (!(y >= -E.nth + margin)) E.refine[d.cand_off + idx] = 1;        // band (or NaN)
+          bool full = false;
+          const unsigned char fl = (sm.ovf[p] == it + 1 || sm.broken)
+                                       ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
+          if (fl) E.refine[d.cand_off + idx] = fl;               // band / range guard / audit
+          if (fl != 1 && full) E.dead[d.ray_off + idx / E.M] = 1;  // certainly full
         }
       }
       st_signal(&sm.cE);

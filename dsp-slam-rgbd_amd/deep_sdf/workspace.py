@@ -79,7 +79,7 @@ class Decoder:
     ``Optimizer`` / ``MeshExtractor``; ``code_len`` and ``layers`` are informative.
     """
 
-    def __init__(self, specs, layers, device=None):
+    def __init__(self, specs, layers, device=None, ctx=None):
         import ctypes as C
 
         from reconstruct import _libdsr as L
@@ -88,7 +88,7 @@ class Decoder:
         self.specs = specs
         self.code_len = specs["CodeLength"]
         self.layers = layers
-        self.ctx = L.Context.get(device)
+        self.ctx = ctx if ctx is not None else L.Context.get(device)   # ctx: an explicit context
         desc = L.DecoderDesc()
         desc.code_len = self.code_len
         desc.n_layers = len(layers)

@@ -57,12 +57,17 @@ class ObjectOut(C.Structure):
                 ("iters_done", C.c_int), ("n_valid_last", C.c_int), ("k_last", C.c_int)]
 
 
+class PoseIn(C.Structure):
+    _fields_ = [("t_co_se3", C.c_float * 16), ("scale", C.c_float), ("pts", FP), ("n_pts", C.c_int),
+                ("code", FP)]
+
+
 class Trace(C.Structure):
     _fields_ = [("H", FP), ("b", FP), ("dx", FP), ("loss", FP), ("sdf_loss", FP),
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 4          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 5          # include/dsr.h DSR_ABI_VERSION
 
 
 class Stats(C.Structure):
@@ -71,7 +76,10 @@ class Stats(C.Structure):
                 ("fwd_launches", C.c_int), ("jac_launches", C.c_int), ("inball_points", C.c_int64),
                 ("lite", C.c_int), ("refine_launches", C.c_int), ("refine_ms", C.c_double),
                 ("refine_points", C.c_int64), ("lite_max_err", C.c_double),
-                ("lite_min_margin", C.c_double)]
+                ("lite_min_margin", C.c_double), ("jac_surface_points", C.c_int64),
+                ("jac_render_points", C.c_int64), ("keep_masks", C.c_int),
+                ("lite_audit_violations", C.c_int), ("lite_redo_objects", C.c_int),
+                ("pad_", C.c_int), ("audit_points", C.c_int64)]
 
 
 #: every function declared in include/dsr.h, with its ctypes signature
@@ -92,12 +100,18 @@ SIGNATURES = {
     "dsr_batch_run": (C.c_int, [C.c_void_p]),
     "dsr_batch_graph": (C.c_int, [C.c_void_p]),
     "dsr_batch_sync": (C.c_int, [C.c_void_p]),
+    "dsr_batch_query": (C.c_int, [C.c_void_p]),
     "dsr_batch_download": (C.c_int, [C.c_void_p, C.POINTER(ObjectOut)]),
     "dsr_batch_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "dsr_batch_destroy": (C.c_int, [C.c_void_p]),
     "dsr_sdf_eval": (C.c_int, [C.c_void_p, C.c_void_p, FP, FP, C.c_int, FP, FP]),
     "dsr_pose_only": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), FP, C.c_float,
                                 FP, C.c_int, FP, FP]),
+    "dsr_pose_only_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int,
+                                      C.POINTER(PoseIn), FP]),
+    "dsr_reconstruct_multi": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
+                                        C.POINTER(OptimParams), C.c_int, C.POINTER(ObjectIn),
+                                        C.POINTER(ObjectOut)]),
     "dsr_mesher_create": (C.c_int, [C.c_void_p, C.c_void_p, FP, C.c_int, C.POINTER(C.c_void_p)]),
     "dsr_mesher_run": (C.c_int, [C.c_void_p, FP, C.c_float, FP, C.c_int, IP, C.c_int, IP, IP]),
     "dsr_mesher_destroy": (C.c_int, [C.c_void_p]),

@@ -15,8 +15,8 @@ runs in libdsr's HIP kernels on an MI355X (``include/dsr.h``):
 * ``Optimizer.compute_sdf_loss_objectpoint_zhjd(pts_obj, code)`` —
   optimizer.py:207-213 -> ``dsr_sdf_eval``.
 * ``Optimizer.estimate_pose_cam_obj(...)`` — optimizer.py:46-87 -> ``dsr_pose_only``.
-* ``MeshExtractor`` — optimizer.py:216-233 (grid decode on device; marching cubes
-  is a §8f follow-on).
+* ``MeshExtractor`` — optimizer.py:216-233 -> ``dsr_mesher_*`` (grid decode and
+  marching cubes on device).
 
 There is no CPU fallback: without libdsr / a gfx950 device these raise DsrError.
 """
@@ -32,6 +32,15 @@ from reconstruct import _libdsr as L
 from reconstruct.utils import ForceKeyErrorDict, create_voxel_grid
 
 _VERBOSE = os.environ.get("DSR_VERBOSE", "0") != "0"
+
+
+def _code(code, code_len):
+    """``code[:code_len]`` as a contiguous float32 vector; the C side reads exactly
+    code_len floats, so a shorter array is an error, never an out-of-bounds read."""
+    c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1)[:code_len])
+    if c.shape[0] != code_len:
+        raise ValueError(f"code must hold at least {code_len} values, got {c.shape[0]}")
+    return c
 
 
 def _f32(a, shape_tail=None):
@@ -80,11 +89,7 @@ class Optimizer(object):
         depth = np.ascontiguousarray(np.asarray(depth, np.float32).reshape(-1))
         if depth.shape[0] > rays.shape[0]:
             raise ValueError("depth holds more values than there are rays")
-        c = None
-        if code is not None:
-            c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1)[:self.code_len])
-            if c.shape[0] != self.code_len:
-                raise ValueError(f"code must hold {self.code_len} values")
+        c = None if code is None else _code(code, self.code_len)
         keep.extend([pts, rays, depth, c])
         rec = L.ObjectIn()
         rec.t_cam_obj[:] = t.reshape(-1).tolist()
@@ -153,11 +158,34 @@ class Optimizer(object):
             return res, bufs
         return res
 
+    def reconstruct_objects_async(self, objects):
+        """Start ``reconstruct_objects(objects)`` and return at once with a
+        :class:`BatchHandle`: the inputs are uploaded (dsr_batch_create), the whole GN run is
+        enqueued on the device (dsr_batch_run) and the host is free — e.g. for the
+        LocalMapping thread's bundle adjustment, which the reference runs after the
+        reconstructions (LocalMapping.cc:99-128) — until ``handle.wait()``."""
+        return BatchHandle(self, objects)
+
+    def reconstruct_keyframe_async(self, detections):
+        """One keyframe's object reconstructions (LocalMapping_util.cc:165-206, 394-410) as
+        ONE asynchronous batched call.  ``detections``: list of ``(t_cam_obj, pts, rays,
+        depth, code, reconstructed)``.  For a detection whose object is not yet
+        reconstructed the reference also runs the left-right flipped hypothesis —
+        ``Sim3Two`` with columns 0 and 2 negated, i.e. ``t_cam_obj @ diag(-1, 1, -1, 1)``
+        (exact in fp32) — and keeps it when the original's loss is larger
+        (LocalMapping_util.cc:400-410; a failed run's loss takes part in that comparison as
+        it does there).  Both hypotheses go into the same batch; ``wait()`` applies the
+        choice and returns one result per detection."""
+        return KeyframeHandle(self, detections)
+
+    def reconstruct_keyframe(self, detections):
+        return self.reconstruct_keyframe_async(detections).wait()
+
     def estimate_pose_cam_obj(self, t_co_se3, scale, pts, code):
         """optimizer.py:46-87: pose-only SE(3) GN on the SDF term."""
         t = _f32(t_co_se3).reshape(4, 4)
         pts = _f32(pts, 3)
-        c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1)[:self.code_len])
+        c = _code(code, self.code_len)
         out = np.zeros((4, 4), np.float32)
         ctx = self._ctx
         ctx.check(ctx.lib.dsr_pose_only(ctx.handle, self.decoder.handle, C.byref(self.params),
@@ -165,20 +193,169 @@ class Optimizer(object):
                                         L.fptr(c), L.fptr(out)), "dsr_pose_only")
         return out
 
+    def estimate_pose_cam_obj_batch(self, objects):
+        """Batched ``estimate_pose_cam_obj``: ``objects`` is a list of
+        ``(t_co_se3, scale, pts, code)``; every object's pose-only GN runs in one device
+        pass per iteration (dsr_pose_only_batch).  The stereo path calls the single form
+        once per associated object per keyframe (LocalMapping_util.cc:103-110)."""
+        n = len(objects)
+        if n == 0:
+            return []
+        keep = []
+        ins = (L.PoseIn * n)()
+        for i, (t, scale, pts, code) in enumerate(objects):
+            t = _f32(t).reshape(4, 4)
+            pts = _f32(pts, 3)
+            c = _code(code, self.code_len)
+            keep += [pts, c]
+            rec = L.PoseIn()
+            rec.t_co_se3[:] = t.reshape(-1).tolist()
+            rec.scale = float(scale)
+            rec.pts, rec.n_pts = L.fptr(pts), pts.shape[0]
+            rec.code = L.fptr(c)
+            ins[i] = rec
+        out = np.zeros((n, 4, 4), np.float32)
+        ctx = self._ctx
+        ctx.check(ctx.lib.dsr_pose_only_batch(ctx.handle, self.decoder.handle, C.byref(self.params), n,
+                                              ins, L.fptr(out)), "dsr_pose_only_batch")
+        return [out[i] for i in range(n)]
+
+    def reconstruct_objects_multi(self, objects, decoders):
+        """``reconstruct_objects`` spread over several devices from ONE process
+        (dsr_reconstruct_multi): ``decoders`` holds one decoder handle per device (e.g.
+        ``[decoder_from_state(state, specs, device=g) for g in range(n)]``); objects are
+        LPT-partitioned, each device's shard runs on its own host thread.  One process
+        per GPU over RCCL is reconstruct.parallel.reconstruct_sharded."""
+        n = len(objects)
+        if n == 0:
+            return []
+        keep = []
+        ins = (L.ObjectIn * n)()
+        for i, ob in enumerate(objects):
+            ins[i] = self._object_in(*ob[:4], ob[4] if len(ob) > 4 else None, keep)
+        outs = (L.ObjectOut * n)()
+        nd = len(decoders)
+        ctxs = (C.c_void_p * nd)(*[d.ctx.handle.value for d in decoders])
+        decs = (C.c_void_p * nd)(*[d.handle.value for d in decoders])
+        ctx = decoders[0].ctx
+        ctx.check(ctx.lib.dsr_reconstruct_multi(ctxs, decs, nd, C.byref(self.params), n, ins, outs),
+                  "dsr_reconstruct_multi")
+        res = [self._result(outs[i]) for i in range(n)]
+        for i in range(n):
+            res[i]["iters_done"] = int(outs[i].iters_done)
+            res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")
+        return res
+
     def compute_sdf_loss_objectpoint_zhjd(self, pts_surface_obj, code):
         """optimizer.py:207-213: mean decoder SDF of object-frame points."""
-        sdf = sdf_eval(self.decoder, code[:self.code_len], pts_surface_obj)
+        sdf = sdf_eval(self.decoder, _code(code, self.code_len), pts_surface_obj)
         mean_value = np.float32(np.mean(sdf)) if sdf.size else np.float32(np.nan)
         if _VERBOSE:
             print("[mapobject sdf loss]python:", mean_value)
         return float(mean_value)
 
 
+class BatchHandle:
+    """An in-flight batched reconstruction (Optimizer.reconstruct_objects_async)."""
+
+    def __init__(self, opt, objects):
+        self.opt = opt
+        self.n = len(objects)
+        self._h = None
+        self._res = None
+        if self.n == 0:
+            self._res = []
+            return
+        keep = []
+        ins = (L.ObjectIn * self.n)()
+        for i, ob in enumerate(objects):
+            ins[i] = opt._object_in(*ob[:4], ob[4] if len(ob) > 4 else None, keep)
+        ctx = opt._ctx
+        h = C.c_void_p()
+        ctx.check(ctx.lib.dsr_batch_create(ctx.handle, opt.decoder.handle, C.byref(opt.params), self.n,
+                                           ins, C.byref(h)), "dsr_batch_create")
+        self._h = h
+        # DSR_GRAPH=1: the whole GN run is captured as one hipGraph and replayed
+        # (dsr_batch_graph is a no-op otherwise)
+        ctx.check(ctx.lib.dsr_batch_graph(h), "dsr_batch_graph")
+        ctx.check(ctx.lib.dsr_batch_run(h), "dsr_batch_run")
+
+    def done(self) -> bool:
+        """True once the device has finished (never blocks)."""
+        if self._res is not None:
+            return True
+        ctx = self.opt._ctx
+        rc = ctx.lib.dsr_batch_query(self._h)
+        if rc < 0:
+            ctx.check(rc, "dsr_batch_query")
+        return rc == 1
+
+    def wait(self):
+        """Block until the run finishes; the list of result dicts, like reconstruct_objects."""
+        if self._res is None:
+            ctx = self.opt._ctx
+            outs = (L.ObjectOut * self.n)()
+            try:
+                ctx.check(ctx.lib.dsr_batch_download(self._h, outs), "dsr_batch_download")
+            finally:
+                ctx.lib.dsr_batch_destroy(self._h)
+                self._h = None
+            res = [Optimizer._result(outs[i]) for i in range(self.n)]
+            for i in range(self.n):
+                res[i]["iters_done"] = int(outs[i].iters_done)
+                res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")
+            self._res = res
+        return self._res
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None:
+            try:
+                self.opt._ctx.lib.dsr_batch_destroy(h)
+            except Exception:
+                pass
+
+
+FLIP = np.diag(np.array([-1.0, 1.0, -1.0, 1.0], np.float32))
+
+
+class KeyframeHandle:
+    """In-flight keyframe batch (Optimizer.reconstruct_keyframe_async)."""
+
+    def __init__(self, opt, detections):
+        objs, self.pairs = [], []
+        for det in detections:
+            t, pts, rays, depth = det[:4]
+            code = det[4] if len(det) > 4 else None
+            done = bool(det[5]) if len(det) > 5 else False
+            i = len(objs)
+            objs.append((t, pts, rays, depth, code))
+            j = None
+            if not done:
+                j = len(objs)
+                objs.append((np.asarray(t, np.float32).reshape(4, 4) @ FLIP, pts, rays, depth, code))
+            self.pairs.append((i, j))
+        self.batch = BatchHandle(opt, objs)
+
+    def done(self) -> bool:
+        return self.batch.done()
+
+    def wait(self):
+        res = self.batch.wait()
+        out = []
+        for i, j in self.pairs:
+            r = res[i]
+            if j is not None and float(r["loss"]) > float(res[j]["loss"]):
+                r = res[j]
+            out.append(r)
+        return out
+
+
 def sdf_eval(decoder, code, pts, with_jac=False):
     """decode_sdf / get_batch_sdf_jacobian (loss_utils.py:51-113) on device."""
     ctx = decoder.ctx
     pts = _f32(pts, 3)
-    c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1))
+    c = _code(code, decoder.code_len)
     n = pts.shape[0]
     sdf = np.zeros(n, np.float32)
     jac = np.zeros((n, c.shape[0] + 3), np.float32) if with_jac else None
@@ -223,17 +400,13 @@ class MeshExtractor(object):
 
     def decode_grid(self, code):
         """The (voxels_dim^3,) SDF grid of optimizer.py:226 (decode_sdf on device)."""
-        return sdf_eval(self.decoder, np.asarray(code)[:self.code_len], self.voxel_points)
+        return sdf_eval(self.decoder, _code(code, self.code_len), self.voxel_points)
 
     def extract_mesh_from_code(self, code, level=0.0):
         ctx = self.decoder.ctx
-        c = np.ascontiguousarray(np.asarray(code, np.float32).reshape(-1)[:self.code_len])
+        c = _code(code, self.code_len)
         nv, nf = C.c_int(), C.c_int()
         ctx.check(ctx.lib.dsr_mesher_run(self._h, L.fptr(c), float(level), L.fptr(self._verts),
                                          self._verts.shape[0], L.iptr(self._faces), self._faces.shape[0],
                                          C.byref(nv), C.byref(nf)), "dsr_mesher_run")
         return ForceKeyErrorDict(vertices=self._verts[:nv.value].copy(), faces=self._faces[:nf.value].copy())
-
-        sdf = self.decode_grid(code).reshape(self.voxels_dim, self.voxels_dim, self.voxels_dim)
-        vertices, faces = marching_cubes_lewiner_like(sdf)
-        return ForceKeyErrorDict(vertices=vertices.astype("float32"), faces=faces.astype("int32"))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 4
+#define DSR_ABI_VERSION 5
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -128,8 +128,19 @@ typedef struct {
   int refine_launches;
   double refine_ms;
   int64_t refine_points;
-  double lite_max_err;            /* max |lite - exact| over the re-decoded samples, all objects */
+  double lite_max_err;            /* max |lite - exact| over the re-decoded samples (band and
+                                     audited), all objects */
   double lite_min_margin;         /* smallest classification margin the last run used */
+  int64_t jac_surface_points;     /* of jac_points: surface points N (forward + backward) */
+  int64_t jac_render_points;      /* of jac_points: render points K (backward only when
+                                     keep_masks, else forward + backward) */
+  int keep_masks;                 /* 1: render points reuse the exact pass's ReLU masks */
+  int lite_audit_violations;      /* audited out-of-band samples whose exact class (full /
+                                     band / empty) differed from the lite pass's */
+  int lite_redo_objects;          /* objects that discarded an iteration for a violation and
+                                     finished with exact decoding */
+  int pad_;
+  int64_t audit_points;           /* out-of-band samples re-decoded exactly as an audit */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */
@@ -163,6 +174,8 @@ int dsr_batch_run(dsr_batch* b);                  /* async on the context stream
                                                       DSR_GRAPH=1 re-runs replay a hipGraph */
 int dsr_batch_graph(dsr_batch* b);                /* capture that graph now (DSR_GRAPH=1) */
 int dsr_batch_sync(dsr_batch* b);
+int dsr_batch_query(dsr_batch* b);                /* 1: the last run has finished, 0: still in
+                                                      flight (host work can overlap it), <0 error */
 int dsr_batch_download(dsr_batch* b, dsr_object_out* out);
 int dsr_batch_stats(dsr_batch* b, dsr_stats* st);
 int dsr_batch_destroy(dsr_batch* b);
@@ -190,12 +203,35 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
                    int fcap, int* n_verts, int* n_faces);
 int dsr_mesher_destroy(dsr_mesher* m);
 
+/* ---- multi-GPU from one process: replaces the per-detection loop
+ * LocalMapping_util.cc:165-206 spread over devices.  ctx[g] / dec[g] are one context and
+ * its decoder per device; objects are LPT-partitioned (cost n_rays*M + n_pts), each
+ * device's shard runs on its own host thread through dsr_reconstruct_batch, and out[] is
+ * filled in input order (results bitwise equal to a one-device batch).  One process per
+ * GPU over RCCL is the Python route (reconstruct/parallel.py). */
+int dsr_reconstruct_multi(dsr_ctx* const* ctx, const dsr_decoder* const* dec, int n_dev,
+                          const dsr_optim_params* p, int n_obj, const dsr_object_in* in,
+                          dsr_object_out* out);
+
 /* ---- pose-only SE(3) GN: replaces Optimizer.estimate_pose_cam_obj
  * (optimizer.py:46-87).  t_co_se3: 4x4 SE(3) camera<-object, scale: object scale,
  * result written to t_out (4x4). */
 int dsr_pose_only(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
                   const float* t_co_se3, float scale, const float* pts, int n_pts,
                   const float* code, float* t_out);
+
+/* Batched form for the stereo path's per-keyframe loop over associated objects
+ * (LocalMapping_util.cc:103-110 calls estimate_pose_cam_obj once per object): every
+ * object's pose-only GN in one device pass per iteration.  t_out: n_obj x 16. */
+typedef struct {
+  float t_co_se3[16];             /* SE(3) camera<-object */
+  float scale;
+  const float* pts;               /* (n_pts,3) camera frame */
+  int n_pts;
+  const float* code;              /* (code_len,) */
+} dsr_pose_in;
+int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
+                        int n_obj, const dsr_pose_in* in, float* t_out);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,14 @@ from gen_mc_tables import build as _build_tables, edge_corners  # noqa: E402
 _COUNTS, _TRIS = _build_tables()
 
 
+def vertex_transform(pos, d):
+    """Grid-index positions (V, 3) float64 -> vertices: skimage's ``index * spacing``
+    (spacing 2/(d-1) in float64), the reference's origin shift (utils.py:131-138) in
+    float64, then ``astype(float32)`` (optimizer.py:228).  Pinned by golden F9."""
+    spacing = 2.0 / (d - 1)                                     # utils.py:127 (float64)
+    return (-1.0 + np.asarray(pos, np.float64) * spacing).astype(np.float32)
+
+
 def marching_cubes(vol, level=0.0):
     """vol: (d, d, d) float32 indexed [i][j][k] = value at grid point (x_i, y_j, z_k).
     Returns vertices (V, 3) float32 in [-1, 1]^3 and faces (F, 3) int32, ordered like the
@@ -51,7 +59,7 @@ def marching_cubes(vol, level=0.0):
     t = (np.float64(lev) - v0) / (v1 - v0)                      # fp64 like skimage's Cython
     base = np.stack([i, j, k], 1).astype(np.float64)
     pos = base + step * t[:, None]
-    verts[:] = (-1.0 + pos * spacing).astype(np.float32)        # utils.py:128-138, optimizer.py:229
+    verts[:] = vertex_transform(pos, d)                           # utils.py:128-138, optimizer.py:228
     # cells
     c = np.arange((d - 1) ** 3)
     ci, cj, ck = c // ((d - 1) ** 2), (c // (d - 1)) % (d - 1), c % (d - 1)

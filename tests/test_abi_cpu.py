@@ -40,12 +40,12 @@ def test_library_exports_every_declared_symbol():
                          text=True, check=True).stdout
     for f in fns:
         assert re.search(rf"\bT {f}$", out, flags=re.M), f
-    assert lib.dsr_abi_version() == 4
+    assert lib.dsr_abi_version() == L.ABI_VERSION
 
 
 STRUCTS = {"dsr_decoder_desc": "DecoderDesc", "dsr_optim_params": "OptimParams",
            "dsr_object_in": "ObjectIn", "dsr_object_out": "ObjectOut", "dsr_trace": "Trace",
-           "dsr_stats": "Stats"}
+           "dsr_stats": "Stats", "dsr_pose_in": "PoseIn"}
 
 
 def test_struct_layouts_match_ctypes():

@@ -1,0 +1,197 @@
+"""Entry points beyond the single-object loop, on the GPU through the C ABI.
+
+* ``dsr_pose_only_batch`` (Optimizer.estimate_pose_cam_obj_batch): the stereo path's
+  per-keyframe loop over associated objects (reference LocalMapping_util.cc:103-110) in
+  one device pass per iteration — bitwise the single-object results, and the F7 golden.
+* ``dsr_reconstruct_multi`` (Optimizer.reconstruct_objects_multi): objects LPT-sharded
+  over several contexts from one process, one host thread per context — bitwise the
+  one-context batch.  Two contexts on device 0 exercise the threading and the gather.
+* edge cases of optimizer.py:90-205: zero iterations (the loop body never runs: input
+  pose / code back, is_good, loss 0.), and the K = 0 exit (golden F6 "bigcode": no
+  render point -> mean of nothing -> NaN -> is_good False, loss of the previous
+  iteration = 0.).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import synthetic as S
+from conftest import golden, make_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def _opt(dec, optim, data_type="KITTI", iters=None):
+    from reconstruct.optimizer import Optimizer
+
+    if iters is not None:
+        optim = dict(optim, joint_optim=dict(optim["joint_optim"], num_iterations=iters))
+    return Optimizer(dec, make_cfg(optim, data_type))
+
+
+def _pose_cases():
+    f = golden("f7_secondary.npz")
+    cases = [(f["t_se3"], float(f["scale"]), f["pts"], f["code"])]
+    rng = np.random.default_rng(3)
+    for i, n in enumerate((100, 700, 1500)):
+        ob = S.kitti_object(20 + i, n_pts=n)
+        T = ob.t_cam_obj.copy()
+        s = float(np.cbrt(np.linalg.det(T[:3, :3].astype(np.float64))))
+        T[:3, :3] /= s
+        cases.append((T, s, ob.pts, (0.05 * rng.standard_normal(64)).astype(np.float32)))
+    return cases
+
+
+@pytest.mark.parametrize("iters", [5, 7])
+def test_pose_only_batch_equals_single(gpu_decoder, iters):
+    optim = dict(S.KITTI_OPTIM, pose_only_optim={"num_iterations": iters, "learning_rate": 1.0})
+    opt = _opt(gpu_decoder, optim)
+    cases = _pose_cases()
+    batch = opt.estimate_pose_cam_obj_batch(cases)
+    for i, c in enumerate(cases):
+        single = opt.estimate_pose_cam_obj(*c)
+        assert np.array_equal(batch[i], single), i
+    if iters == 5:
+        f = golden("f7_secondary.npz")
+        assert np.abs(batch[0] - f["pose_only_out"]).max() <= 2e-5 * np.abs(f["pose_only_out"]).max()
+
+
+def test_reconstruct_multi_equals_one_context(gpu_decoder, full_layers):
+    from deep_sdf.workspace import Decoder
+    from reconstruct import _libdsr as L
+
+    ctx2 = L.Context(0)                      # a second context on the same device
+    dec2 = Decoder(S.DEFAULT_SPECS, full_layers, ctx=ctx2)
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=3)
+    objs = []
+    for i in range(7):
+        o = S.make_object(700 + i, n_pts=150 + 61 * i, n_bg=20 + 9 * i, scale=1.0, tz=3.0, upright=False)
+        objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
+    one = opt.reconstruct_objects(objs)
+    multi = opt.reconstruct_objects_multi(objs, [gpu_decoder, dec2])
+    for a, b in zip(one, multi):
+        assert a["is_good"] == b["is_good"]
+        assert a["loss"] == b["loss"]
+        if a["is_good"]:
+            assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"])
+            assert np.array_equal(a["code"], b["code"])
+
+
+def test_zero_iterations_returns_input(gpu_decoder):
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=0)
+    ob = S.redwood_object(0, n_pts=128)
+    warm = np.linspace(-0.1, 0.1, 64).astype(np.float32)
+    for code in (None, warm):
+        r = opt.reconstruct_object(ob.t_cam_obj, ob.pts, ob.rays, ob.depth, code)
+        assert r["is_good"] and r["loss"] == 0.0 and r["iters_done"] == 0
+        # inverse(inverse(T)) in fp32, like the reference's optimizer.py:105-106, :202
+        assert np.abs(r["t_cam_obj"] - ob.t_cam_obj).max() <= 1e-5 * np.abs(ob.t_cam_obj).max()
+        assert np.array_equal(r["code"], np.zeros(64, np.float32) if code is None else warm)
+
+
+def test_no_render_points_is_a_failure(gpu_decoder):
+    f = golden("f6_fail.npz")
+    assert list(f["bigcode_k"]) == [0]       # the reference's own K = 0 case
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")
+    r = opt.reconstruct_object(f["obj_t_cam_obj"], f["obj_pts"], f["obj_rays"], f["obj_depth"],
+                               f["bigcode"])
+    assert r["is_good"] is False and r["t_cam_obj"] is None and r["code"] is None
+    assert r["loss"] == float(f["bigcode_loss"]) == 0.0
+    assert r["fail_reason"] == "render loss is NaN (no render points)"
+    assert r["iters_done"] == 0
+
+
+def test_keyframe_batch_async_graph(gpu_decoder, oracle_dec, monkeypatch):
+    """BASELINE config 5: one keyframe's detections with their flipped hypotheses
+    (LocalMapping_util.cc:394-410) in ONE asynchronous batch — under DSR_GRAPH=1 the whole
+    GN run is one replayed hipGraph — while the host keeps working; results equal the
+    eager batch bitwise, the lower-loss hypothesis is kept, and every object's first GN
+    step matches the oracle's from the same state."""
+    from oracle import dsr_oracle as O
+    from reconstruct.optimizer import FLIP
+
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")
+    obs = [S.redwood_object(40 + i) for i in range(4)]
+    dets = [(o.t_cam_obj, o.pts, o.rays, o.depth, None, False) for o in obs]
+    eager = opt.reconstruct_keyframe(dets)
+    monkeypatch.setenv("DSR_GRAPH", "1")
+    h = opt.reconstruct_keyframe_async(dets)
+    host_work = 0
+    while not h.done():                        # the LocalMapping thread's BA would run here
+        host_work += 1
+    res = h.wait()
+    assert host_work > 0
+    for a, b in zip(eager, res):
+        assert a["is_good"] == b["is_good"] and a["loss"] == b["loss"]
+        if a["is_good"]:
+            assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"]) and np.array_equal(a["code"], b["code"])
+    # the choice rule, against the two hypotheses run separately
+    both = opt.reconstruct_objects([x for o in obs for x in ((o.t_cam_obj, o.pts, o.rays, o.depth, None),
+                                                              (o.t_cam_obj @ FLIP, o.pts, o.rays, o.depth,
+                                                               None))])
+    for i, r in enumerate(res):
+        a, b = both[2 * i], both[2 * i + 1]
+        assert r["loss"] == (b["loss"] if a["loss"] > b["loss"] else a["loss"])
+    # first GN step of all 8 hypotheses vs the oracle from the same state
+    monkeypatch.delenv("DSR_GRAPH")
+    one = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=1)
+    objs = [x for o in obs for x in ((o.t_cam_obj, o.pts, o.rays, o.depth, None),
+                                     (o.t_cam_obj @ FLIP, o.pts, o.rays, o.depth, None))]
+    r1, t1 = one.reconstruct_objects(objs, trace=True)
+    P = O.OptimParams.from_cfg(S.REDWOOD_OPTIM)
+    for i, (T, pts, rays, depth, _) in enumerate(objs):
+        n_fg = depth.shape[0]
+        dobs = np.concatenate([depth, np.zeros(rays.shape[0] - n_fg)]).astype(np.float32)
+        tro, _, _ = O.gn_step(oracle_dec, P, np.linalg.inv(T), np.zeros(64, np.float32), pts, rays,
+                              dobs, n_fg)
+        assert abs(int(t1[i]["k"][0]) - tro.k) <= 2, i
+        assert abs(t1[i]["sdf_loss"][0] - tro.sdf_loss) <= 5e-5 * abs(tro.sdf_loss), i
+        flips = max(abs(int(t1[i]["k"][0]) - tro.k), 2)
+        assert abs(t1[i]["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
+                                                                  + flips * 0.09 / tro.k), i
+        H = np.asarray(tro.H, np.float64)
+        assert np.abs(t1[i]["H"][0] - H).max() <= 5e-3 * np.abs(H).max(), i
+
+
+def test_entry_path_as_the_cpp_side_calls_it(gpu_decoder, full_state, tmp_path):
+    """System.cc:95-98 then LocalMapping.cc:38-40: get_configs -> get_decoder ->
+    Optimizer(decoder, cfg) and MeshExtractor(decoder, cfg.optimizer.code_len,
+    cfg.voxels_dim), on a DeepSDF experiment directory (specs.json + latest.pth)."""
+    from test_host_cpu import _reference_style_config
+
+    from reconstruct.optimizer import MeshExtractor, Optimizer, sdf_eval
+    from reconstruct.utils import get_configs, get_decoder
+
+    exp = S.write_experiment_dir(str(tmp_path / "deepsdf"), full_state)
+    cfg = get_configs(_reference_style_config(tmp_path, exp))
+    dec = get_decoder(cfg)
+    opt = Optimizer(dec, cfg)
+    mex = MeshExtractor(dec, cfg.optimizer.code_len, cfg.voxels_dim)
+    assert opt.code_len == 64
+    rng = np.random.default_rng(8)
+    z = (0.1 * rng.standard_normal(64)).astype(np.float32)
+    x = rng.uniform(-0.9, 0.9, (500, 3)).astype(np.float32)
+    y1, j1 = sdf_eval(dec, z, x, with_jac=True)
+    y0, j0 = sdf_eval(gpu_decoder, z, x, with_jac=True)
+    assert np.array_equal(y1, y0) and np.array_equal(j1, j0)
+    ob = S.redwood_object(3, n_pts=256)
+    r1 = opt.reconstruct_object(ob.t_cam_obj, ob.pts, ob.rays, ob.depth)
+    r0 = Optimizer(gpu_decoder, cfg).reconstruct_object(ob.t_cam_obj, ob.pts, ob.rays, ob.depth)
+    assert r1["is_good"] and r1["loss"] == r0["loss"]
+    assert np.array_equal(r1["t_cam_obj"], r0["t_cam_obj"]) and np.array_equal(r1["code"], r0["code"])
+    mesh = mex.extract_mesh_from_code(r1["code"])
+    assert mesh.vertices.dtype == np.float32 and mesh.faces.dtype == np.int32 and len(mesh.faces) > 0
+
+
+def test_mesher_grid_decode_vs_reference_f9(gpu_decoder):
+    """The device grid decode of MeshExtractor vs the volume the reference hands to
+    marching cubes (golden F9, optimizer.py:225-227), same tolerance as the decoder F1."""
+    from reconstruct.optimizer import MeshExtractor
+
+    f = golden("f9_mesher.npz")
+    d = int(f["dim"])
+    mex = MeshExtractor(gpu_decoder, 64, d)
+    assert np.array_equal(mex.voxel_points, f["grid"])
+    vol = mex.decode_grid(f["code"]).reshape(d, d, d)
+    assert np.abs(vol - f["volume"]).max() <= 2e-5

@@ -1,0 +1,144 @@
+"""The lite classification pass is guarded, not trusted.
+
+The one-product fp16 pass (dsr_mlp_lite.hpp) only has to tell, for every ray sample,
+whether its sdf is certainly >= th (empty), certainly <= -th (full) or possibly in the
+band (loss_utils.py:40-48, loss.py:101-102); the band is re-decoded exactly.  Its
+margin calibrates itself from measured errors, and every iteration an AUDIT re-decodes
+exactly the out-of-band samples within th + 1.5*margin plus a hashed 1/128 of all others
+(dsr_dev.hpp: lite_flag).  Their error feeds the calibration; a class disagreement on
+any of them discards that object's iteration and redoes it, and the rest of the run,
+with every sample decoded exactly (k_solve, k_iter_begin).
+
+These tests (1) force violations with a deterministic perturbation of every lite value
+(DSR_LITE_PERTURB) and show the guard fires and the results equal exact decoding
+(DSR_LITE=0) at the teacher-forced tolerances; (2) check later iterations — where the
+margin has calibrated down to its 0.005 floor — against exact decoding from the same
+state, on the bench decoder and on a decoder with larger hidden weights (larger
+activations, larger fp16 error).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import synthetic as S
+from conftest import golden, make_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def _opt(dec, optim, data_type="KITTI", iters=None):
+    from reconstruct.optimizer import Optimizer
+
+    if iters is not None:
+        optim = dict(optim, joint_optim=dict(optim["joint_optim"], num_iterations=iters))
+    return Optimizer(dec, make_cfg(optim, data_type))
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def batch_stats(opt, objects, pose_is_obj_cam=False):
+    """Run ``objects`` through the resident-batch API; return (outs, dsr_stats)."""
+    from reconstruct import _libdsr as L
+
+    keep = []
+    n = len(objects)
+    ins = (L.ObjectIn * n)()
+    for i, ob in enumerate(objects):
+        ins[i] = opt._object_in(*ob[:4], ob[4] if len(ob) > 4 else None, keep, pose_is_obj_cam)
+    ctx = opt._ctx
+    h = C.c_void_p()
+    ctx.check(ctx.lib.dsr_batch_create(ctx.handle, opt.decoder.handle, C.byref(opt.params), n, ins,
+                                       C.byref(h)), "create")
+    try:
+        outs = (L.ObjectOut * n)()
+        ctx.check(ctx.lib.dsr_batch_run(h), "run")
+        ctx.check(ctx.lib.dsr_batch_download(h, outs), "download")
+        st = L.Stats()
+        ctx.check(ctx.lib.dsr_batch_stats(h, C.byref(st)), "stats")
+    finally:
+        ctx.lib.dsr_batch_destroy(h)
+    return outs, st
+
+
+def assert_same_step(t1, t0, e1=0, e0=0, what=""):
+    """One GN iteration's terms agree like the lite-vs-exact A/B of test_gpu_parity."""
+    assert int(t1["n_valid"][e1]) == int(t0["n_valid"][e0]), what
+    assert int(t1["k"][e1]) == int(t0["k"][e0]), what
+    assert abs(t1["loss"][e1] - t0["loss"][e0]) <= 1e-5 * abs(t0["loss"][e0]), what
+    assert rel(t1["H"][e1], t0["H"][e0]) <= 1e-4, what
+    d = np.asarray(t1["dx"][e1], np.float64) - t0["dx"][e0]
+    H = np.asarray(t0["H"][e0], np.float64)
+    dx0 = np.asarray(t0["dx"][e0], np.float64)
+    assert np.sqrt(max(d @ H @ d, 0) / max(dx0 @ H @ dx0, 1e-300)) <= 1e-3, what
+
+
+def test_audit_guard_fires_and_redoes_exactly(gpu_decoder, monkeypatch):
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=1)
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
+            for e in (0, 4, 9)]
+    monkeypatch.setenv("DSR_LITE", "0")
+    r0, t0 = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    monkeypatch.setenv("DSR_LITE", "1")
+    # every lite value off by +-0.025: band samples land in the audit shell th+m..th+1.5m
+    # (first-iteration margin 0.02), so every object sees violations
+    monkeypatch.setenv("DSR_LITE_PERTURB", "0.025")
+    outs, st = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert st.lite == 1 and st.audit_points > 0
+    assert st.lite_audit_violations > 0
+    assert st.lite_redo_objects == len(objs)
+    assert all(outs[i].is_good and outs[i].iters_done == 1 for i in range(len(objs)))
+    r1, t1 = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    for i in range(len(objs)):
+        assert r1[i]["is_good"] and r0[i]["is_good"]
+        assert_same_step(t1[i], t0[i], what=f"object {i}")
+    # without the audit the same perturbation silently changes the render set
+    monkeypatch.setenv("DSR_LITE_AUDIT", "0")
+    r2, t2 = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    assert any(int(t2[i]["k"][0]) != int(t0[i]["k"][0]) for i in range(len(objs)))
+
+
+def test_audit_quiet_and_cheap_on_the_bench_workload(gpu_decoder, monkeypatch):
+    """Unperturbed: no violation, the audit re-decodes a bounded share of the samples."""
+    monkeypatch.setenv("DSR_LITE", "1")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM)
+    objs = [S.kitti_object(i) for i in range(8)]
+    outs, st = batch_stats(opt, [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
+    assert st.lite_audit_violations == 0 and st.lite_redo_objects == 0
+    assert st.audit_points > 0
+    assert st.audit_points <= 0.1 * st.fwd_points, (st.audit_points, st.fwd_points)
+    assert 0.0 < st.lite_max_err < 0.005 / 4
+    assert abs(st.lite_min_margin - 0.005) < 1e-7
+
+
+@pytest.mark.parametrize("gain", [2.45, 3.2], ids=["bench_decoder", "larger_weights"])
+def test_calibrated_margin_iterations_match_exact(gain, monkeypatch):
+    """Iterations 1.. of a lite run (calibrated margin) vs exact decoding from that state."""
+    from deep_sdf.workspace import decoder_from_state
+
+    if gain == 2.45:
+        state = S.make_decoder(1234)
+    else:
+        state = S.fit_last_layer_to_sphere(S.make_decoder_state(1234, hidden_gain=gain))
+    dec = decoder_from_state(state, S.DEFAULT_SPECS)
+    opt = _opt(dec, S.KITTI_OPTIM, iters=4)
+    one = _opt(dec, S.KITTI_OPTIM, iters=1)
+    objs = [S.kitti_object(i) for i in (0, 3)]
+    monkeypatch.setenv("DSR_LITE", "1")
+    res, tr = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs],
+                                      trace=True)
+    outs, st = batch_stats(opt, [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
+    assert st.lite_audit_violations == 0, st.lite_audit_violations
+    for i, o in enumerate(objs):
+        assert res[i]["is_good"]
+        states = [(tr[i]["t_obj_cam"][e], o.pts, o.rays, o.depth, tr[i]["z"][e]) for e in (1, 2, 3)]
+        monkeypatch.setenv("DSR_LITE", "0")
+        r0, t0 = one.reconstruct_objects(states, trace=True, pose_is_obj_cam=True)
+        monkeypatch.setenv("DSR_LITE", "1")
+        for j, e in enumerate((1, 2, 3)):
+            assert_same_step(tr[i], t0[j], e1=e, e0=0, what=f"gain {gain} object {i} iteration {e}")

@@ -3,15 +3,19 @@
 Tolerances:
 * decoder SDF / Jacobian vs golden F1: fp32, |err| <= 2e-5 abs (sdf in (-1,1)),
   <= 1e-4 x max|jac| for the Jacobian (autograd vs analytic backward, fp32 sums);
-* one teacher-forced GN iteration vs golden F4 (same state in): identical N_valid
-  and K, loss rel <= 1e-5, H <= 2e-3, b and dx <= 1e-2 (max-normalised; these
-  sums cancel and carry the ~4e-5 render-Jacobian noise every fp32 implementation
-  has, golden F23);
-* full trajectories: mask flips (|sdf|=th, de_do=1e-2, |x|=1) amplify fp32
-  rounding chaotically — the reference itself moves by up to 1.4e-2 in T between
-  1 and 8 CPU threads (fixtures t4_/t8_).  The trajectory tests therefore check
-  every GPU step against the oracle's step FROM THE GPU'S OWN STATE (shadowing)
-  plus the final loss against the reference within its own spread.
+* one teacher-forced GN iteration vs golden F4 (same state in): N_valid and K within
+  2 (samples within fp32 rounding of |x| = 1 or |sdf| = th flip between any two fp32
+  implementations; the loss bound grows by the most one flipped render point can move
+  it), loss rel <= 1e-5 at identical K, H <= 2e-3, b and dx <= 5e-2 max-normalised and
+  the step <= 1e-2 in the H-norm (b[3:6] carries k4 * J_rot * r_rot with k4 = 1e7 and
+  r_rot an fp32 cancellation quantised in 6e-8 steps, in the reference itself);
+* full trajectories: mask flips (|sdf|=th, de_do=1e-2, |x|=1) and ReLU kinks at the
+  Jacobian points amplify fp32 rounding chaotically — the reference itself moves by
+  up to 4e-1 in its final code under a 1-ulp pose perturbation (F4 ensembles).  The
+  trajectory test therefore checks every GPU step against the oracle's step FROM THE
+  GPU'S OWN STATE (shadowing); the final state is held to the reference in
+  tests/test_gpu_contract.py (strictly on margin-screened inputs, by the reference's
+  own reproducibility envelope on these).
 """
 from __future__ import annotations
 
@@ -134,13 +138,7 @@ def test_trajectory_shadowing_and_final(gpu_decoder, oracle_dec, name, optim, dt
     (r,), (t,) = opt.reconstruct_objects(
         [(f["obj_t_cam_obj"], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)], trace=True)
     assert r["is_good"]
-    # final loss vs the reference, judged against the reference's own spread: its
-    # ensemble (1/2/4/8 threads, 1-ulp pose perturbations) moves the final loss by up to
-    # `dev`; a chaotic fp32 trajectory is accepted within 3 dev (min 1% of the loss).
-    # Per-step correctness is proved below by shadowing, not by this bound.
-    ref = float(f["loss"])
-    dev = float(np.abs(f["ens_loss"] - ref).max())
-    assert abs(r["loss"] - ref) <= max(3 * dev, 0.01 * abs(ref)), (r["loss"], ref, dev)
+    # (final state vs the reference: test_gpu_contract.py)
     # shadowing: the GPU's step e, re-taken from the state the GPU itself reached, vs
     # the oracle's step from that same state
     P = O.OptimParams.from_cfg(optim)
@@ -230,16 +228,32 @@ def test_zhjd_query(gpu_decoder):
     assert abs(v - float(f["zhjd_out"])) <= 2e-6
 
 
-def test_full_size_batch_properties(gpu_decoder):
-    """BASELINE config 3 shape (16 KITTI objects x 2048 pts): all good, finite, and
-    each object's first step matches the oracle's (spot-checked on two objects)."""
+def test_full_size_batch_properties(gpu_decoder, oracle_dec):
+    """BASELINE config 3 shape (16 KITTI objects x 2048 pts): all good, finite, and the
+    first GN step of objects 0 and 11 matches the oracle's from the same state."""
+    from oracle import dsr_oracle as O
+
     opt = _opt(gpu_decoder, S.KITTI_OPTIM, "KITTI")
     objs = [S.kitti_object(i) for i in range(16)]
-    res = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
+    res, tr = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs],
+                                      trace=True)
     assert all(r["is_good"] for r in res)
     for r in res:
         assert np.isfinite(r["t_cam_obj"]).all() and np.isfinite(r["code"]).all()
         assert np.isfinite(r["loss"]) and r["loss"] > 0
+    P = O.OptimParams.from_cfg(S.KITTI_OPTIM)
+    for i in (0, 11):
+        o, t = objs[i], tr[i]
+        n_fg = o.depth.shape[0]
+        dobs = np.concatenate([o.depth, np.zeros(o.rays.shape[0] - n_fg)]).astype(np.float32)
+        tro, _, _ = O.gn_step(oracle_dec, P, t["t_obj_cam"][0], t["z"][0], o.pts, o.rays, dobs, n_fg)
+        assert abs(int(t["k"][0]) - tro.k) <= 2 and abs(int(t["n_valid"][0]) - tro.n_valid) <= 2, i
+        assert abs(t["sdf_loss"][0] - tro.sdf_loss) <= 5e-5 * abs(tro.sdf_loss), i
+        flips = max(abs(int(t["k"][0]) - tro.k), 2)
+        assert abs(t["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
+                                                              + flips * 0.09 / tro.k), i
+        assert rel(t["H"][0], tro.H) <= 5e-3, i
+        assert step_err(t["dx"][0], tro.dx, tro.H) <= 2e-2, i
 
 
 def test_pose_only_vs_golden(gpu_decoder, oracle_dec):

@@ -166,3 +166,32 @@ def test_zhjd_and_pose_only(oracle_dec):
     P = O.OptimParams.from_cfg(S.KITTI_OPTIM)
     T = O.estimate_pose_cam_obj(oracle_dec, P, f["t_se3"], float(f["scale"]), f["pts"], f["code"])
     assert np.abs(T - f["pose_only_out"]).max() <= 1e-4 * np.abs(f["pose_only_out"]).max()
+
+
+def _f8_paths():
+    import glob
+    import os
+
+    from conftest import GOLDEN
+
+    return sorted(glob.glob(os.path.join(GOLDEN, "f8_margin_*.npz")))
+
+
+@pytest.mark.parametrize("path", _f8_paths(), ids=lambda p: p.rsplit("/", 1)[-1][10:-4])
+def test_oracle_final_state_on_margin_fixtures(oracle_dec, path):
+    """The oracle (numpy fp32) meets the north-star output contract against the reference
+    on the margin-screened trajectories (F8, tests/golden/make_margin.py): exact K every
+    iteration, final pose / code <= 1e-3, loss <= 1e-4 relative (optimizer.py:202-205)."""
+    from test_gpu_contract import CODE_TOL, LOSS_TOL, POSE_TOL, contract_errors, optim_of
+
+    f = np.load(path, allow_pickle=False)
+    optim, _ = optim_of(f)
+    P = O.OptimParams.from_cfg(optim)
+    r = O.reconstruct_object(oracle_dec, P, f["obj_t_cam_obj"], f["obj_pts"], f["obj_rays"],
+                             f["obj_depth"])
+    assert r.is_good
+    n_it = int(f["n_iters_run"])
+    assert [tr.k for tr in r.trace] == f["it_k"][:n_it].tolist()
+    e_rot, e_t, e_z, e_l = contract_errors(r.t_cam_obj, r.code, r.loss, f)
+    assert e_rot <= POSE_TOL and e_t <= POSE_TOL and e_z <= CODE_TOL and e_l <= LOSS_TOL, \
+        (e_rot, e_t, e_z, e_l)
