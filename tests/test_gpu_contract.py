@@ -12,15 +12,17 @@ is checked two ways:
 
 * strict, on margin-screened fixtures (F8, tests/golden/make_margin.py): inputs on
   which every iteration keeps every relevant sample >= 1e-5 from each mask threshold
-  AND the reference's own 8-member ulp-perturbation ensemble stays within half the
-  contract — there the build must land on the reference's result: identical K every
+  AND the reference's own 8-member ulp-perturbation ensemble stays within the
+  contract (K identical in every member) — there the build must land on the
+  reference's result: identical K every
   iteration, final pose (rotation·scale block and translation, max-norm relative) and
   code <= 1e-3, loss <= 1e-4, on both decode paths (DSR_LITE=1 default, DSR_LITE=0);
 * by envelope, on the full-size bench objects (F4): the build's deviation from the
-  reference's 1-thread result is no larger than 1.5x the largest deviation of the
-  reference's own ensemble (2/4/8 threads, ulp-perturbed poses), or the contract
-  tolerance where that is larger — i.e. the GPU result is one more member of the
-  reference's own reproducibility cloud, for pose, code and loss alike.
+  reference's 1-thread result is no larger than twice the largest deviation among 16
+  members of the reference's own ensemble (1 thread, initial pose perturbed by one
+  fp32 ulp; tests/golden/make_ensemble.py), or the contract tolerance where that is
+  larger — i.e. the GPU result is one more member of the reference's own
+  reproducibility cloud, for pose, code and loss alike.
 
 The CPU oracle is held to the strict contract on the same F8 fixtures in
 ``tests/test_oracle_golden.py::test_oracle_final_state_on_margin_fixtures``.
@@ -55,7 +57,12 @@ def contract_errors(T, z, loss, f):
 
 
 def optim_of(f):
-    return (S.KITTI_OPTIM, "KITTI") if str(f["data_type"]) == "KITTI" else (S.REDWOOD_OPTIM, "Redwood")
+    """The fixture's parameter set (configs/config_kitti.json / config_redwood_01053.json),
+    with the iteration count it was generated with."""
+    optim, dtp = (S.KITTI_OPTIM, "KITTI") if str(f["data_type"]) == "KITTI" else (S.REDWOOD_OPTIM, "Redwood")
+    if "num_iterations" in f.files:
+        optim = dict(optim, joint_optim=dict(optim["joint_optim"], num_iterations=int(f["num_iterations"])))
+    return optim, dtp
 
 
 def _run(dec, f, optim, dtp):
@@ -120,10 +127,11 @@ def test_full_size_final_state_within_reference_envelope(gpu_decoder, name, opti
     r, _ = _run(gpu_decoder, f, optim, dtp)
     assert r["is_good"]
     gpu = np.array(contract_errors(r["t_cam_obj"], r["code"], r["loss"], f))
-    ens = np.array([contract_errors(f["ens_t_cam_obj"][m], f["ens_code"][m], f["ens_loss"][m], f)
-                    for m in range(len(f["ens_loss"]))])
+    key = "ens16_" if "ens16_loss" in f.files else "ens_"
+    ens = np.array([contract_errors(f[key + "t_cam_obj"][m], f[key + "code"][m], f[key + "loss"][m], f)
+                    for m in range(len(f[key + "loss"]))])
     env = np.nanmax(ens, axis=0)
-    tol = np.maximum([POSE_TOL, POSE_TOL, CODE_TOL, LOSS_TOL], 1.5 * env)
+    tol = np.maximum([POSE_TOL, POSE_TOL, CODE_TOL, LOSS_TOL], 2.0 * env)
     print(f"\n{name}: gpu rot/t/code/loss {np.array2string(gpu, precision=2)} reference ensemble "
           f"{np.array2string(env, precision=2)}")
     assert (gpu <= tol).all(), (gpu, env)

@@ -89,7 +89,8 @@ def test_decoder_vs_oracle_random(gpu_decoder, oracle_dec):
 @pytest.mark.parametrize("name,optim,dtype", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),
                                               ("redwood1", S.REDWOOD_OPTIM, "Redwood"),
                                               ("kitti0", S.KITTI_OPTIM, "KITTI"),
-                                              ("kitti5", S.KITTI_OPTIM, "KITTI")])
+                                              ("kitti5", S.KITTI_OPTIM, "KITTI"),
+                                              ("kitti4096", S.KITTI_OPTIM, "KITTI")])
 def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
     """Every recorded reference state -> one GPU GN step -> H, b, dx, loss, K."""
     f = golden(f"f4_traj_{name}.npz")
