@@ -534,13 +534,13 @@ static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
 }
 
 // Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
-// (1.5): out-of-band samples with |y| < th + shell*margin are audited; DSR_LITE_AUDIT_LOG2
+// (1.0): out-of-band samples with |y| < th + shell*margin are audited; DSR_LITE_AUDIT_LOG2
 // (7): plus a hashed 2^-log2 share of all other decoded samples; DSR_LITE_PERTURB: test hook
 static void lite_audit_args(ErtArgs& E) {
   auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
   const char* a = getenv("DSR_LITE_AUDIT");
   E.audit = (a && atoi(a) == 0) ? 0 : 1;
-  E.shell = envf("DSR_LITE_SHELL", 1.5f);
+  E.shell = envf("DSR_LITE_SHELL", 1.0f);
   E.audit_log2 = std::max(0, std::min(24, (int)envf("DSR_LITE_AUDIT_LOG2", 7.0f)));
   E.perturb = envf("DSR_LITE_PERTURB", 0.0f);
 }
@@ -557,9 +557,11 @@ static GNParams make_params(const dsr_optim_params* p) {
   P.cut_off = p->cut_off; P.iters = p->num_iterations; P.M = p->num_depth_samples;
   P.raw_residual = 0;
   auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
-  P.lite_margin0 = envf("DSR_LITE_MARGIN", 0.02f);    // dsr_mlp_lite.hpp
-  P.lite_floor = envf("DSR_LITE_FLOOR", 0.005f);
-  P.lite_safety = envf("DSR_LITE_SAFETY", 8.0f);
+  // lite-pass margin: th in the first iteration, then max(0.002, 4 x the
+  // largest |lite - exact| the object's band and audit samples showed; the audit guards it)
+  P.lite_margin0 = envf("DSR_LITE_MARGIN", 0.01f);
+  P.lite_floor = envf("DSR_LITE_FLOOR", 0.002f);
+  P.lite_safety = envf("DSR_LITE_SAFETY", 4.0f);
   return P;
 }
 

@@ -549,8 +549,9 @@ def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
     finally:
         lib.dsr_batch_destroy(h)
     assert st.lite == 1 and st.refine_points > 0 and st.refine_launches > 0
-    assert 0.0 < st.lite_max_err < 0.005 / 4           # 4x inside the smallest margin
-    assert abs(st.lite_min_margin - 0.005) < 1e-7      # floor reached after calibration
+    # calibrated margin max(0.002, 4 x the largest observed error), well inside th = 0.01
+    assert 0.0 < st.lite_max_err < 1e-3
+    assert 0.002 - 1e-7 <= st.lite_min_margin <= max(0.002, 4 * st.lite_max_err) + 1e-7
 
 
 @pytest.mark.gpu
