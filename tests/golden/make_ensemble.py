@@ -11,8 +11,9 @@ The spread of the members' final (t_cam_obj, code, loss) around the unperturbed
 the envelope tests/test_gpu_contract.py holds the build to on these full-size objects.
 Arrays added: ens16_t_cam_obj (16,4,4), ens16_code (16,64), ens16_loss (16,),
 ens16_is_good (16,), ens16_k (16, iters); with DSR_ENS_MEMBERS=M the same under the
-prefix ``ens{M}_`` (the first 16 members are the ens16 ones: same perturbation stream),
-members run in DSR_ENS_JOBS forked 1-thread processes.  The maximum deviation of a
+prefix ``ens{M}_`` (the first 16 members get the ens16 perturbations; their results differ
+from ens16's in the last bits — the reference's CPU kernels are not reproducible across
+processes either), members run in DSR_ENS_JOBS forked 1-thread processes.  The maximum deviation of a
 16-member cloud underestimates the cloud's extent; 64 members estimate it better.
 """
 from __future__ import annotations
