@@ -42,7 +42,7 @@ import synthetic as S  # noqa: E402
 FWD_MAC = 1_769_984     # algorithmic forward MACs / point (code broadcast folded), SURVEY §8
 BWD_MAC = 1_835_520     # input-gradient backward MACs / point
 FP16_MFMA_PEAK_TF = 2500.0          # dense fp16/bf16 MFMA, spec (MI355X_MICROARCH.md)
-FP16_MFMA_LOOP_TF = 1247.0          # the guide's bare bf16 MFMA loop on random data (DVFS item 1)
+FP16_MFMA_LOOP_TF = 1247.0          # the guide's bare 32x32x16 bf16 MFMA loop on random data (DVFS item 1)
 SPLIT_PRODUCTS = 3                  # 3xFP16: hi*hi + hi*lo + lo*hi per fp32 product
 DTYPE = ("fp16-mfma: 3xFP16 split (hi/lo fp16, fp32 accumulate) for every value that reaches "
          "an output + one-product fp16 classification of ray samples")
@@ -160,8 +160,8 @@ def kernel_rooflines(a):
     def entry(name, flop, ms, launches, peak, loop, note):
         tf = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         out[name] = {"achieved_tflops": round(tf, 2), "peak_tflops": round(peak, 1),
-                     "frac_of_peak": round(tf / peak, 4), "bare_mfma_loop_tflops": round(loop, 1),
-                     "frac_of_bare_loop": round(tf / loop, 4), "launches": launches,
+                     "frac_of_peak": round(tf / peak, 4), "guide_bf16_loop_tflops": round(loop, 1),
+                     "frac_of_guide_loop": round(tf / loop, 4), "launches": launches,
                      "avg_launch_ms": round(ms / max(1, launches), 5),
                      "flop_per_launch": flop / max(1, launches), "flop_counted": note}
 
@@ -178,6 +178,27 @@ def kernel_rooflines(a):
     entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop,
           "N surface points x 2*(1,769,984+1,835,520) + K render points x 2*"
           + ("1,835,520 (backward only, kept masks)" if a.get("keep_masks") else "(fwd+bwd)"))
+    return out
+
+
+def measured_mfma_loop(device=0, ms=300.0):
+    """The device's bare v_mfma_f32_16x16x32_f16 loop on random register operands, every
+    SIMD busy (csrc/dsr_diag.hip): the fp16 MFMA rate the chip sustains under load on this
+    box (it lowers its clock under MFMA load, MI355X_MICROARCH.md 'DVFS give-back'), for
+    one and two waves per SIMD (the decoder kernels run two).  None if unavailable."""
+    path = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", "libdsr_diag.so")
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    out = {}
+    for w in (1, 2):
+        tf, t = C.c_float(), C.c_float()
+        if lib.dsr_diag_mfma_f16(device, w, 0, C.c_float(ms), C.byref(tf), C.byref(t)) != 0:
+            return None
+        out[f"waves_per_simd_{w}"] = round(tf.value, 1)
+    out["tflops"] = max(out.values())
+    out["note"] = ("bare fp16 MFMA loop (16x16x32, 8 accumulators, random operands in registers, "
+                   "every SIMD busy), measured after the timed region on the same device")
     return out
 
 
@@ -297,6 +318,12 @@ def main():
         elapsed = float(t.item())
     value = n_job * args.steps / elapsed
     roof = kernel_rooflines(acc) if acc else {}
+    loop = measured_mfma_loop(local) if rank == 0 and acc and not args.no_extra else None
+    if loop:
+        for name, e in roof.items():     # the split kernels' fp32-equivalent rate is 1/3 of fp16
+            k = 1.0 if "lite" in name else 1.0 / SPLIT_PRODUCTS
+            e["measured_loop_tflops"] = round(loop["tflops"] * k, 1)
+            e["frac_of_measured_loop"] = round(e["achieved_tflops"] / (loop["tflops"] * k), 4)
     if rank == 0:
         dom = "k_mlp_fwd_lite_st" if acc.get("lite") else "k_mlp_fwd16"
         r = roof.get(dom, {})
@@ -327,6 +354,7 @@ def main():
                          "avg_launch_ms": r.get("avg_launch_ms"), "launches": r.get("launches"),
                          "flop_per_launch": r.get("flop_per_launch")},
             "rooflines": roof,
+            "mfma_loop": loop,
             "early_ray_termination": {"samples_decoded": acc.get("fwd_points"),
                                       "samples_in_ball": acc.get("inball_points"),
                                       "decoded_fraction": round(acc.get("fwd_points", 0)

@@ -205,6 +205,9 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
   const _Float16* Bh = Hh + boff;
   const _Float16* Bl = Hl + boff;
   auto lda = [&](int q, int t, int piece) {
+#ifdef DSR_EXP_NOSTREAM            // timing experiment (invalid results): A from one k step only
+    t = 0;
+#endif
     return __builtin_bit_cast(
         half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, ((q * T + t) * 2 + piece) * 1024, 0));
   };

@@ -43,6 +43,14 @@ def test_library_exports_every_declared_symbol():
     assert lib.dsr_abi_version() == L.ABI_VERSION
 
 
+def test_diag_library_exports_the_mfma_loop():
+    """libdsr_diag.so (bench.py's measured MFMA ceiling) is built beside libdsr.so."""
+    path = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", "libdsr_diag.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    assert re.search(r"\bT dsr_diag_mfma_f16$", out, flags=re.M)
+
+
 STRUCTS = {"dsr_decoder_desc": "DecoderDesc", "dsr_optim_params": "OptimParams",
            "dsr_object_in": "ObjectIn", "dsr_object_out": "ObjectOut", "dsr_trace": "Trace",
            "dsr_stats": "Stats", "dsr_pose_in": "PoseIn"}
