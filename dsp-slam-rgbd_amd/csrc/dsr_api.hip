@@ -168,6 +168,9 @@ struct dsr_batch {
   int* is_oc = nullptr;
   float *pts = nullptr, *rays = nullptr, *dobs = nullptr;
   float4 *cand = nullptr, *kpts = nullptr;
+  float4* kst = nullptr;           // k_render_rays staging (per chunk, at its rays' sample range)
+  float* rst = nullptr;
+  int* sst = nullptr;
   float *dense = nullptr, *kres = nullptr;
   float *bias0f = nullptr, *bias4f = nullptr;
   // Object groups: contiguous object ranges whose GN iterations run on their own streams,
@@ -179,6 +182,9 @@ struct dsr_batch {
     Tile *tiles_f = nullptr, *tiles_j = nullptr;
     int *nt_f = nullptr, *nt_j = nullptr;
     unsigned* sync = nullptr;
+    RenderChunk* rchunks = nullptr;   // k_render_rays chunks of the group's objects
+    int* ccnt = nullptr;              // render points per chunk
+    int n_rch = 0;
   };
   std::vector<Group> groups;
   hipEvent_t fork_ev = nullptr;
@@ -239,6 +245,10 @@ int dsr_ctx_create(int device, dsr_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) return -4;
+  // k_render_rays' dynamic LDS reaches 66.5 KB at the largest sample count (M = 64)
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_render_rays), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)render_lds_bytes(MAXM)) != hipSuccess)
+    return -1;
   auto* c = new dsr_ctx();
   c->device = device;
   c->n_cu = prop.multiProcessorCount;
@@ -684,6 +694,9 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     }
   }
   ALLOC(b->kres, sizeof(float) * (size_t)cand_off);
+  ALLOC(b->kst, sizeof(float4) * (size_t)cand_off);
+  ALLOC(b->rst, sizeof(float) * (size_t)cand_off);
+  if (b->kslot) ALLOC(b->sst, sizeof(int) * (size_t)cand_off);
   ALLOC(b->bias0f, sizeof(float) * HID * n_obj);
   ALLOC(b->bias4f, sizeof(float) * HID * n_obj);
   for (auto& gr : b->groups) {
@@ -696,6 +709,18 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ALLOC(gr.nt_f, sizeof(int));
     ALLOC(gr.nt_j, sizeof(int));
     ALLOC(gr.sync, 8 * 32 * sizeof(unsigned));
+    std::vector<RenderChunk> rch;
+    for (int o = gr.o0; o < gr.o0 + gr.n; ++o) {
+      const int first = (int)rch.size(), nch = (b->hdesc[o].n_rays + RENDER_RAYS - 1) / RENDER_RAYS;
+      for (int c = 0; c < nch; ++c) rch.push_back(RenderChunk{o - gr.o0, c * RENDER_RAYS, first, nch});
+    }
+    gr.n_rch = (int)rch.size();
+    ALLOC(gr.rchunks, sizeof(RenderChunk) * rch.size());
+    ALLOC(gr.ccnt, sizeof(int) * rch.size());
+    if (hipMemcpy(gr.rchunks, rch.data(), sizeof(RenderChunk) * rch.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      dsr_batch_destroy(b);
+      return fail(ctx, "hipMemcpy (render chunks) failed");
+    }
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
   b->loop_iters = b->iters + ((b->lite && lite_audit_on() && b->iters > 0) ? 1 : 0);
@@ -939,8 +964,11 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       }
       const bool keep = b->lite && b->ma.msk && fv == 12;
       const int je = 2 * (np + (b->lite ? 1 : 0));
-      hipLaunchKernelGGL(k_render, dim3(ng), dim3(RENDER_THREADS), 0, s, ng, desc, st, b->rays, b->dobs, P,
-                         b->dense, b->kpts, b->kres, (const int*)b->ma.slotmap, keep ? b->kslot : nullptr);
+      hipLaunchKernelGGL(k_render_rays, dim3(gr.n_rch), dim3(RENDER_RAYS), render_lds_bytes(b->M), s,
+                         gr.rchunks, desc, st, b->rays, b->dobs, P, b->dense, b->kst, b->rst,
+                         keep ? b->sst : nullptr, (const int*)b->ma.slotmap, gr.ccnt);
+      hipLaunchKernelGGL(k_render_gather, dim3(gr.n_rch), dim3(256), 0, s, gr.rchunks, desc, st, gr.ccnt, b->M,
+                         b->kst, b->rst, b->sst, b->kpts, b->kres, keep ? b->kslot : nullptr);
       hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,

@@ -656,11 +656,27 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
 }
 
 // ------------------------------------------------------------------------------------
-// k_render: per-ray occupancy scan (loss.py:97-150), one 512-thread workgroup per object,
-// one thread per ray; the per-ray transmittance row lives in LDS (pitch MAXM+1: the
-// threads of a wave hit 64 different banks), occupancies are re-derived from `dense`.
+// k_render_rays + k_render_gather: the per-ray occupancy scan of loss.py:97-150 and the
+// ordered compaction of its K render points.  One thread per ray; an object's rays are
+// split into chunks of RENDER_RAYS, one workgroup each (the table is built once per batch),
+// so the ~5-20 chunks of an object run side by side instead of one workgroup walking the
+// rays in rounds (a per-object latency that small batches cannot hide: 179 -> ~40 us per
+// KITTI object).  Each chunk stages its rays' sdf rows in LDS twice (coalesced loads): the
+// scan turns one copy into the transmittance rows, the other keeps the sdf values the
+// de_do filter needs (no global re-reads inside the per-ray loops).  A chunk writes its
+// render points, in (ray, depth) order, to a staging area at its own rays' sample range and
+// its count; k_render_gather moves every chunk's points to the object's compacted K list
+// at the sum of the earlier chunks' counts — the same list, in the same order, as one
+// sequential pass over the rays.
 // ------------------------------------------------------------------------------------
-constexpr int RENDER_THREADS = 512;
+constexpr int RENDER_RAYS = 128;
+
+struct RenderChunk {
+  int obj;        // object index within the launch
+  int ray0;       // first ray of the chunk (object-local)
+  int first;      // launch-table index of the object's first chunk
+  int n;          // chunks of the object
+};
 
 __device__ __forceinline__ float occupancy(float s, float nth, float th, float two_th) {
   // sdf_to_occupancy (loss_utils.py:40-48); NaN marks a sample outside the unit ball
@@ -669,110 +685,143 @@ __device__ __forceinline__ float occupancy(float s, float nth, float th, float t
   return 0.5f - fminf(fmaxf(s, nth), th) / two_th;
 }
 
-__global__ __launch_bounds__(RENDER_THREADS) void k_render(int n_obj, const ObjDesc* __restrict__ desc,
-                                                           ObjState* st, const float* __restrict__ rays_all,
-                                                           const float* __restrict__ dobs_all, GNParams P,
-                                                           const float* __restrict__ dense,
-                                                           float4* __restrict__ kpts,
-                                                           float* __restrict__ kres,
-                                                           const int* __restrict__ slotmap,
-                                                           int* __restrict__ kslot) {
-  const int o = blockIdx.x;
-  ObjState& S = st[o];
+// LDS row pitch of the per-ray rows: odd, so the 64 lanes of a wave hit 64 different banks
+__host__ __device__ constexpr int render_pitch(int M) { return (M + 1) | 1; }
+__host__ __device__ constexpr size_t render_lds_bytes(int M) {
+  return sizeof(float) * 2 * RENDER_RAYS * (size_t)render_pitch(M);
+}
+
+__global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* __restrict__ chunks,
+                                                             const ObjDesc* __restrict__ desc,
+                                                             const ObjState* __restrict__ st,
+                                                             const float* __restrict__ rays_all,
+                                                             const float* __restrict__ dobs_all, GNParams P,
+                                                             const float* __restrict__ dense,
+                                                             float4* __restrict__ kst, float* __restrict__ rst,
+                                                             int* __restrict__ sst, const int* __restrict__ slotmap,
+                                                             int* __restrict__ ccnt) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  const ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
-  const ObjDesc d = desc[o];
-  const int M = P.M;
+  const ObjDesc d = desc[ch.obj];
+  const int M = P.M, pitch = render_pitch(M);
   const float th = P.cut_off;
   const float nth = -th, two_th = 2.0f * th;
   const float do_ds = (float)(-1.0 / (2.0 * (double)th));
-  const float* rays = rays_all + (size_t)d.ray_off * 3;
-  __shared__ float T_s[RENDER_THREADS * (MAXM + 1)];
+  extern __shared__ float render_lds[];
+  float* T_s = render_lds;                       // transmittance rows (sdf until scanned)
+  float* D_s = render_lds + RENDER_RAYS * pitch;  // sdf rows
   __shared__ float dep_s[MAXM];
-  __shared__ int wsum[RENDER_THREADS / 64];
-  __shared__ int base_s;
+  __shared__ int wsum[RENDER_RAYS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) base_s = 0;
   if (tid < M) dep_s[tid] = S.depths[tid];
+  const int nr = min(RENDER_RAYS, d.n_rays - ch.ray0);
+  {
+    const float* src = dense + d.cand_off + (size_t)ch.ray0 * M;
+    for (int e = tid; e < nr * M; e += RENDER_RAYS) {
+      const int r = e / M, j = e - r * M;
+      const float v = src[e];
+      T_s[r * pitch + j] = v;
+      D_s[r * pitch + j] = v;
+    }
+  }
   __syncthreads();
   const float dmax = S.dmax, delta_d = S.delta_d;
-  float* Tr = T_s + tid * (MAXM + 1);
-  for (int r0 = 0; r0 < d.n_rays; r0 += RENDER_THREADS) {
-    const int ray = r0 + tid;
-    int cnt = 0, jend = 0;
-    float du = 0.f, dob = 0.f;
-    uint64_t keep = 0;
-    const float* sd = dense + d.cand_off + (size_t)ray * M;
-    {   // the round's sdf rows, coalesced, into the transmittance rows (each scan reads
-        // sample j before overwriting it with T_j); the per-ray scans then wait on LDS only
-      const int nr = min(RENDER_THREADS, d.n_rays - r0);
-      const float* src = dense + d.cand_off + (size_t)r0 * M;
-      for (int e = tid; e < nr * M; e += RENDER_THREADS) T_s[(e / M) * (MAXM + 1) + e % M] = src[e];
-      __syncthreads();
+  const int ray = ch.ray0 + tid;
+  float* Tr = T_s + tid * pitch;
+  const float* Dr = D_s + tid * pitch;
+  int cnt = 0, jend = 0;
+  float du = 0.f, dob = 0.f;
+  uint64_t keep = 0;
+  if (tid < nr) {
+    // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
+    // probabilities and rendered depth (:112-125).  The 51-term sum is accumulated in
+    // fp64 and rounded once: torch's vectorised fp32 sum is within ~1 ulp of exact,
+    // a sequential fp32 sum is not (d ~ 15 m, residual d_obs - d_u ~ 1 cm).
+    // Once T == 0 (a sample with occupancy exactly 1) every later term probability,
+    // transmittance and de_do is an exact 0: the scan stops there — the samples behind
+    // were not decoded (early ray termination, k_sample_pass) and cannot matter.
+    uint64_t grad = 0;
+    float T = 1.f;
+    double dud = 0.0;
+    int j = 0;
+    for (; j < M && T != 0.f; ++j) {
+      const float s = Tr[j];
+      const float ov = occupancy(s, nth, th, two_th);
+      if (s > nth && s < th) grad |= 1ull << j;     // loss.py:101
+      const float tp = ov * T;
+      T = T * (1.f - ov);
+      Tr[j] = T;
+      dud += (double)(dep_s[j] * tp);
     }
-    if (ray < d.n_rays) {
-      // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
-      // probabilities and rendered depth (:112-125).  The 51-term sum is accumulated in
-      // fp64 and rounded once: torch's vectorised fp32 sum is within ~1 ulp of exact,
-      // a sequential fp32 sum is not (d ~ 15 m, residual d_obs - d_u ~ 1 cm).
-      // Once T == 0 (a sample with occupancy exactly 1) every later term probability,
-      // transmittance and de_do is an exact 0: the scan stops there — the samples behind
-      // were not decoded (early ray termination, k_sample_pass) and cannot matter.
-      uint64_t grad = 0;
-      float T = 1.f;
-      double dud = 0.0;
-      int j = 0;
-      for (; j < M && T != 0.f; ++j) {
-        const float s = Tr[j];                       // = sd[j] (staged above)
-        const float ov = occupancy(s, nth, th, two_th);
-        if (s > nth && s < th) grad |= 1ull << j;     // loss.py:101
-        const float tp = ov * T;
-        T = T * (1.f - ov);
-        Tr[j] = T;
-        dud += (double)(dep_s[j] * tp);
-      }
-      jend = j;                                       // Tr[l] = 0 for l >= jend
-      dud += (double)((1.1f * dmax) * T);            // background bin o=1, d=1.1*d_max
-      du = (float)dud;
-      dob = dobs_all[d.ray_off + ray];
-      for (uint64_t m = grad; m; m &= m - 1) {
-        const int jj = __builtin_ctzll(m);
-        double sacc = 0.0;
-        for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
-        const float dedo = (float)sacc / (1.f - occupancy(sd[jj], nth, th, two_th));   // :131-132
-        if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; }                              // :135
-      }
+    jend = j;                                       // Tr[l] = 0 for l >= jend
+    dud += (double)((1.1f * dmax) * T);            // background bin o=1, d=1.1*d_max
+    du = (float)dud;
+    dob = dobs_all[d.ray_off + ray];
+    for (uint64_t m = grad; m; m &= m - 1) {
+      const int jj = __builtin_ctzll(m);
+      double sacc = 0.0;
+      for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
+      const float dedo = (float)sacc / (1.f - occupancy(Dr[jj], nth, th, two_th));   // :131-132
+      if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; }                              // :135
     }
-    const int inc = wave_incl_scan(cnt, lane);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int off = base_s + inc - cnt;
-    for (int k = 0; k < wv; ++k) off += wsum[k];
-    if (cnt > 0) {
-      float res = dob - du;                           // :145
-      res = res > 0.30f ? 0.30f : res;                // :147-148
-      res = res < -0.30f ? -0.30f : res;
-      for (uint64_t m = keep; m; m &= m - 1) {
-        const int jj = __builtin_ctzll(m);
-        double sacc = 0.0;
-        for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
-        const float dedo = (float)sacc / (1.f - occupancy(sd[jj], nth, th, two_th));
-        const float deds = (dedo * delta_d) * do_ds;    // :142
-        const float3 x = ray_sample(rays, S, ray, jj);
-        kpts[d.cand_off + off] = make_float4(x.x, x.y, x.z, deds);
-        kres[d.cand_off + off] = res;
-        if (kslot) kslot[d.cand_off + off] = slotmap[d.cand_off + ray * M + jj];
-        ++off;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int t = 0;
-      for (int k = 0; k < RENDER_THREADS / 64; ++k) t += wsum[k];
-      base_s += t;
-    }
-    __syncthreads();
   }
-  if (tid == 0) S.k = base_s;
+  const int inc = wave_incl_scan(cnt, lane);
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int off = inc - cnt;
+  for (int k = 0; k < wv; ++k) off += wsum[k];
+  if (cnt > 0) {
+    float res = dob - du;                           // :145
+    res = res > 0.30f ? 0.30f : res;                // :147-148
+    res = res < -0.30f ? -0.30f : res;
+    const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
+    const float rx = rp[0], ry = rp[1], rz = rp[2];
+    const size_t base = (size_t)d.cand_off + (size_t)ch.ray0 * M;
+    for (uint64_t m = keep; m; m &= m - 1) {
+      const int jj = __builtin_ctzll(m);
+      double sacc = 0.0;
+      for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
+      const float dedo = (float)sacc / (1.f - occupancy(Dr[jj], nth, th, two_th));
+      const float deds = (dedo * delta_d) * do_ds;    // :142
+      const float dj = dep_s[jj];
+      const float3 x = xform(S.T, rx * dj, ry * dj, rz * dj);   // = ray_sample(rays, S, ray, jj)
+      kst[base + off] = make_float4(x.x, x.y, x.z, deds);
+      rst[base + off] = res;
+      if (sst) sst[base + off] = slotmap[d.cand_off + ray * M + jj];
+      ++off;
+    }
+  }
+  if (tid == 0) {
+    int t = 0;
+    for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
+    ccnt[blockIdx.x] = t;
+  }
+}
+
+// Every chunk's render points to the object's K list (offset = the earlier chunks' counts);
+// the object's last chunk sets K.
+__global__ __launch_bounds__(256) void k_render_gather(const RenderChunk* __restrict__ chunks,
+                                                       const ObjDesc* __restrict__ desc, ObjState* st,
+                                                       const int* __restrict__ ccnt, int M,
+                                                       const float4* __restrict__ kst,
+                                                       const float* __restrict__ rst,
+                                                       const int* __restrict__ sst, float4* __restrict__ kpts,
+                                                       float* __restrict__ kres, int* __restrict__ kslot) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  ObjState& S = st[ch.obj];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[ch.obj];
+  int off = 0;
+  for (int c = ch.first; c < (int)blockIdx.x; ++c) off += ccnt[c];
+  const int n = ccnt[blockIdx.x];
+  if (threadIdx.x == 0 && (int)blockIdx.x == ch.first + ch.n - 1) S.k = off + n;
+  const size_t s0 = (size_t)d.cand_off + (size_t)ch.ray0 * M, d0 = (size_t)d.cand_off + off;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    kpts[d0 + i] = kst[s0 + i];
+    kres[d0 + i] = rst[s0 + i];
+    if (kslot) kslot[d0 + i] = sst[s0 + i];
+  }
 }
 
 // ------------------------------------------------------------------------------------
