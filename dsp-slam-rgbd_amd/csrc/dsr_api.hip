@@ -118,7 +118,7 @@ static LiteKernel lite_kernel() {
   return k_mlp_fwd_lite_st<true, 88 + 256 + 1024>;
 }
 // DSR_REFINE_ALL=1: the exact pass re-decodes every band sample, also those behind a ray's
-// first certainly-full sample (k_refine_compact)
+// first certainly-full sample (k_refine_scan)
 static bool refine_all() {
   const char* e = getenv("DSR_REFINE_ALL");
   return e && atoi(e) != 0;
@@ -191,6 +191,7 @@ struct dsr_batch {
   hipEvent_t done_ev = nullptr;  // recorded after every run (dsr_batch_query)
   std::vector<hipEvent_t> join_ev;
   float* slots = nullptr;
+  float* sred = nullptr;        // [n_obj][2][SLOT_FLOATS] tile-partial sums (k_reduce_slots)
   int* counts = nullptr;
   dsr_object_out* out = nullptr;
   float *tr_H = nullptr, *tr_v = nullptr;
@@ -198,6 +199,7 @@ struct dsr_batch {
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
   int* rinfo = nullptr;         // per-ray in-ball run (first in-ball sample | count << 8), or -1
   unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
+  uint64_t *rbits = nullptr, *abits = nullptr;   // per-ray refined / audited sample bits (k_refine_scan)
   MaskArgs ma{nullptr, nullptr, nullptr, nullptr};   // kept masks of the exact re-decode
   int* kslot = nullptr;
   bool lite = true;             // lite classification pass + exact re-decode of the band
@@ -688,6 +690,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
       b->ma.kslot = b->kslot;
     }
     ALLOC(b->refine, (size_t)std::max(1, cand_off));
+    ALLOC(b->rbits, sizeof(uint64_t) * (size_t)std::max(1, ray_off));
+    ALLOC(b->abits, sizeof(uint64_t) * (size_t)std::max(1, ray_off));
     if (hipMemset(b->refine, 0, (size_t)std::max(1, cand_off)) != hipSuccess) {
       dsr_batch_destroy(b);
       return fail(ctx, "hipMemset failed");
@@ -723,6 +727,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     }
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
+  ALLOC(b->sred, sizeof(float) * 2 * SLOT_FLOATS * (size_t)n_obj);
   b->loop_iters = b->iters + ((b->lite && lite_audit_on() && b->iters > 0) ? 1 : 0);
   ALLOC(b->counts, sizeof(int) * NCOUNT * (size_t)std::max(1, b->loop_iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
@@ -949,8 +954,10 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       if (b->lite) {                             // exact split-fp16 decode of the band samples
         if (b->ma.slotmap)
           DSR_CHECK(ctx, hipMemsetAsync(b->ma.slotmap + gr.c0, 0xff, sizeof(int) * (size_t)(gr.c1 - gr.c0), s));
-        hipLaunchKernelGGL(k_refine_compact, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->cand, b->refine, b->ma.slotmap, refine_all() ? nullptr : b->dense, -P.cut_off);
+        hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->M,
+                           b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt);
+        hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                           b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
@@ -978,7 +985,9 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
       hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
                          b->counts + (size_t)o0 * NCOUNT, n);
-      hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, b->slots,
+      float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
+      hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred);
+      hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, sred,
                          b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
                          b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
                          b->tr_i ? b->tr_i + (size_t)o0 * 2 : nullptr, n);

@@ -85,7 +85,7 @@ struct ObjState {
   int n_refine;          // of which re-decoded exactly after the lite pass
   float lite_margin;     // this iteration's classification margin (dsr_mlp_lite.hpp)
   float lite_err;        // max |lite - exact| seen on this object's re-decoded samples
-  int n_audit;           // this iteration's audited out-of-band samples (k_refine_compact)
+  int n_audit;           // this iteration's audited out-of-band samples (k_refine_scan)
   int lite_viol;         // this iteration's audited samples whose exact class differs
   int lite_viol_total;   // over the run
   int lite_redo;         // 1: an iteration was discarded for a violation; exact from then on
@@ -117,7 +117,7 @@ struct ErtArgs {
 constexpr int AUDIT_BIT = 1 << 30;
 
 // Lite-pass classification of one decoded sample (lite value y, index idx = ray*M + j)
-// into the refine flags k_refine_compact consumes: 1 = band (|y| < th + margin, NaN, or
+// into the refine flags k_refine_scan consumes: 1 = band (|y| < th + margin, NaN, or
 // the range guard), 2 = audited certainly-empty sample, 3 = audited certainly-full sample
 // (3 also terminates the ray, like an unaudited full sample).  Returns the flag (0: none)
 // and sets `full` when the sample is certainly full.

@@ -294,6 +294,17 @@ __device__ __forceinline__ float3 ray_sample(const float3 r, const SampleLds& L,
 // and counts n_valid (loss.py:82-88) over ALL in-ball samples.
 // One thread per ray, one workgroup per object, (ray, depth)-ordered output.
 // ------------------------------------------------------------------------------------
+// Ray chunks: k_refine_* and k_render_* run one workgroup per RENDER_RAYS rays of an object
+// (table built once per batch), so an object's rays are processed side by side.
+constexpr int RENDER_RAYS = 128;
+
+struct RenderChunk {
+  int obj;        // object index within the launch
+  int ray0;       // first ray of the chunk (object-local)
+  int first;      // launch-table index of the object's first chunk
+  int n;          // chunks of the object
+};
+
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -406,9 +417,12 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
 }
 
 // ------------------------------------------------------------------------------------
-// k_refine_compact: the samples the lite pass left in the +-(th + margin) band
-// (dsr_mlp_lite.hpp), (ray, depth)-ordered into cand for the exact split-fp16 pass;
-// clears the flags it consumes.  One thread per ray, one workgroup per object.
+// k_refine_scan + k_refine_emit: the samples the lite pass left in the +-(th + margin) band
+// (dsr_mlp_lite.hpp), (ray, depth)-ordered into cand for the exact split-fp16 pass; the
+// scan clears the flags it consumes.  One thread per ray, one workgroup per chunk of
+// RENDER_RAYS rays (the render chunk table): the scan records each ray's refined and
+// audited sample bits and the chunk's count; the emit places every chunk at the sum of the
+// earlier chunks' counts — the list one sequential pass over the rays would build.
 // A ray's scan stops at its first certainly-full sample (an unflagged lite value
 // <= -th - margin, the criterion that set `dead`): its exact sdf is <= -th, so the
 // transmittance is exactly 0 behind it and every later sample enters d_u, de_do and K
@@ -418,88 +432,118 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
 // samples hold NaN, so the scan reads only this iteration's values.  `dense` == nullptr
 // refines every flagged sample (DSR_REFINE_ALL=1).
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(SAMPLE_THREADS) void k_refine_compact(int n_obj, const ObjDesc* __restrict__ desc,
-                                                                   ObjState* st, const float* __restrict__ rays_all,
-                                                                   int M, float4* __restrict__ cand,
-                                                                   unsigned char* __restrict__ refine,
-                                                                   int* __restrict__ slotmap,
-                                                                   const float* __restrict__ dense, float nth) {
-  const int o = blockIdx.x;
-  ObjState& S = st[o];
+__global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* __restrict__ chunks,
+                                                             const ObjDesc* __restrict__ desc, ObjState* st,
+                                                             int M, unsigned char* __restrict__ refine,
+                                                             const float* __restrict__ dense, float nth,
+                                                             uint64_t* __restrict__ rbits_g,
+                                                             uint64_t* __restrict__ abits_g, int* __restrict__ ccnt) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
-  const ObjDesc d = desc[o];
-  const float* rays = rays_all + (size_t)d.ray_off * 3;
-  __shared__ int wsum[SAMPLE_THREADS / 64];
-  __shared__ int base_s;
+  const ObjDesc d = desc[ch.obj];
+  __shared__ uint64_t rbits[RENDER_RAYS], abits[RENDER_RAYS];
+  __shared__ int wsum[RENDER_RAYS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) base_s = 0;
-  __syncthreads();
-  __shared__ uint64_t rbits[SAMPLE_THREADS], abits[SAMPLE_THREADS];
   const float full = nth - S.lite_margin;
-  int n_audit = 0;
-  for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
-    const int ray = r0 + tid;
-    // Each wave scans 64 rays one at a time, lane j on sample j (coalesced flag / value
-    // loads, ballots): refined = the flagged samples in front of the first unflagged sample
-    // that is certainly full, or up to and including it when it is an audited full sample
-    // (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag) ride along in bit 30 of
-    // the candidate's index so the exact pass can check their class.
-    for (int i0 = 0; i0 < 64; i0 += 8) {     // 8 rays' loads in flight
-      unsigned char fv[8];
-      float yv[8];
+  // Each wave scans its 64 rays one at a time, lane j on sample j (coalesced flag / value
+  // loads, ballots): refined = the flagged samples in front of the first unflagged sample
+  // that is certainly full, or up to and including it when it is an audited full sample
+  // (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag) ride along in bit 30 of
+  // the candidate's index so the exact pass can check their class.
+  for (int i0 = 0; i0 < 64; i0 += 8) {     // 8 rays' loads in flight
+    unsigned char fv[8];
+    float yv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int rr = r0 + 64 * wv + i0 + u;
-        const bool in = rr < d.n_rays && lane < M;
-        const size_t e = d.cand_off + (size_t)rr * M + lane;
-        fv[u] = in ? refine[e] : 0;
-        yv[u] = (in && dense) ? dense[e] : __builtin_nanf("");
+    for (int u = 0; u < 8; ++u) {
+      const int rr = ch.ray0 + 64 * wv + i0 + u;
+      const bool in = rr < d.n_rays && lane < M;
+      const size_t e = d.cand_off + (size_t)rr * M + lane;
+      fv[u] = in ? refine[e] : 0;
+      yv[u] = (in && dense) ? dense[e] : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int rr = ch.ray0 + 64 * wv + i0 + u;
+      const uint64_t fb = __ballot(fv[u] != 0);
+      const uint64_t ub = __ballot((fv[u] == 0 || fv[u] == 3) && yv[u] <= full);
+      const uint64_t tb = __ballot(fv[u] == 3), ab = __ballot(fv[u] >= 2);
+      uint64_t b = fb;
+      if (ub) {
+        const int stop = __builtin_ctzll(ub);
+        b = fb & (((1ull << stop) - 1) | (tb & (1ull << stop)));
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int rr = r0 + 64 * wv + i0 + u;
-        const uint64_t fb = __ballot(fv[u] != 0);
-        const uint64_t ub = __ballot((fv[u] == 0 || fv[u] == 3) && yv[u] <= full);
-        const uint64_t tb = __ballot(fv[u] == 3), ab = __ballot(fv[u] >= 2);
-        uint64_t b = fb;
-        if (ub) {
-          const int stop = __builtin_ctzll(ub);
-          b = fb & (((1ull << stop) - 1) | (tb & (1ull << stop)));
-        }
-        if (rr < d.n_rays && lane < M) refine[d.cand_off + (size_t)rr * M + lane] = 0;
-        if (lane == i0 + u) {
-          rbits[tid] = b;
-          abits[tid] = b & ab;
-        }
+      if (rr < d.n_rays && lane < M) refine[d.cand_off + (size_t)rr * M + lane] = 0;
+      if (lane == i0 + u) {
+        rbits[tid] = b;
+        abits[tid] = b & ab;
       }
     }
-    const uint64_t bits = rbits[tid], aud = abits[tid];
-    const int cnt = __popcll(bits);
-    n_audit += __popcll(aud);
-    const int inc = wave_incl_scan(cnt, lane);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int off = base_s + inc - cnt;
-    for (int k = 0; k < wv; ++k) off += wsum[k];
-    for (uint64_t m = bits; m; m &= m - 1) {
-      const int j = __builtin_ctzll(m);
-      const float3 x = ray_sample(rays, S, ray, j);
-      if (slotmap) slotmap[d.cand_off + ray * M + j] = off;
-      const int tag = ((aud >> j) & 1) ? AUDIT_BIT : 0;
-      cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float((ray * M + j) | tag));
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int t = 0;
-      for (int k = 0; k < SAMPLE_THREADS / 64; ++k) t += wsum[k];
-      base_s += t;
-    }
-    __syncthreads();
   }
+  const uint64_t bits = rbits[tid], aud = abits[tid];
+  const int ray = ch.ray0 + tid;
+  if (ray < d.n_rays) {
+    rbits_g[d.ray_off + ray] = bits;
+    abits_g[d.ray_off + ray] = aud;
+  }
+  const int n_audit = __popcll(aud);
   if (n_audit) atomicAdd(&S.n_audit, n_audit);
+  int cnt = __popcll(bits);
+#pragma unroll
+  for (int k = 32; k > 0; k >>= 1) cnt += __shfl_xor(cnt, k);
+  if (lane == 0) wsum[wv] = cnt;
+  __syncthreads();
   if (tid == 0) {
-    S.n_emit = base_s;
-    S.n_refine = base_s;
+    int t = 0;
+    for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
+    ccnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(RENDER_RAYS) void k_refine_emit(const RenderChunk* __restrict__ chunks,
+                                                             const ObjDesc* __restrict__ desc, ObjState* st,
+                                                             const float* __restrict__ rays_all, int M,
+                                                             float4* __restrict__ cand, int* __restrict__ slotmap,
+                                                             const uint64_t* __restrict__ rbits_g,
+                                                             const uint64_t* __restrict__ abits_g,
+                                                             const int* __restrict__ ccnt) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  ObjState& S = st[ch.obj];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[ch.obj];
+  __shared__ int wsum[RENDER_RAYS / 64];
+  __shared__ SampleLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  stage_samples(L, S, M, tid);
+  int base = 0;
+  for (int c = ch.first; c < (int)blockIdx.x; ++c) base += ccnt[c];
+  const int ray = ch.ray0 + tid;
+  uint64_t bits = 0, aud = 0;
+  float3 rv = make_float3(0.f, 0.f, 0.f);
+  if (ray < d.n_rays) {
+    bits = rbits_g[d.ray_off + ray];
+    aud = abits_g[d.ray_off + ray];
+    const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
+    rv = make_float3(rp[0], rp[1], rp[2]);
+  }
+  const int cnt = __popcll(bits);
+  const int inc = wave_incl_scan(cnt, lane);
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int off = base + inc - cnt;
+  for (int k = 0; k < wv; ++k) off += wsum[k];
+  for (uint64_t m = bits; m; m &= m - 1) {
+    const int j = __builtin_ctzll(m);
+    const float3 x = ray_sample(rv, L, j);
+    if (slotmap) slotmap[d.cand_off + ray * M + j] = off;
+    const int tag = ((aud >> j) & 1) ? AUDIT_BIT : 0;
+    cand[d.cand_off + off++] = make_float4(x.x, x.y, x.z, __int_as_float((ray * M + j) | tag));
+  }
+  if (tid == 0 && (int)blockIdx.x == ch.first + ch.n - 1) {
+    int t = base;
+    for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
+    S.n_emit = t;
+    S.n_refine = t;
   }
 }
 
@@ -669,14 +713,6 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
 // at the sum of the earlier chunks' counts — the same list, in the same order, as one
 // sequential pass over the rays.
 // ------------------------------------------------------------------------------------
-constexpr int RENDER_RAYS = 128;
-
-struct RenderChunk {
-  int obj;        // object index within the launch
-  int ray0;       // first ray of the chunk (object-local)
-  int first;      // launch-table index of the object's first chunk
-  int n;          // chunks of the object
-};
 
 __device__ __forceinline__ float occupancy(float s, float nth, float th, float two_th) {
   // sdf_to_occupancy (loss_utils.py:40-48); NaN marks a sample outside the unit ball
@@ -1350,11 +1386,46 @@ __device__ __forceinline__ float quad_bcast(float v, int k) {
 constexpr int SOLVE_THREADS = 320;   // 5 waves: substitutions run 4 lanes per column
 constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render, T, z
 
+// k_reduce_slots: the per-tile normal-equation partials of each object summed in tile order
+// (sdf tiles, render tiles: two fp64 sums per element, rounded once), one thread per element
+// and SLOT_BLOCKS workgroups per object, 8 tiles' loads in flight per thread — the same
+// sums, in the same order, as one workgroup walking the tiles, without that walk's ~90
+// dependent memory latencies per object.  red[o][0][e] = sdf sums, red[o][1][e] = render.
+constexpr int SLOT_BLOCKS = (SLOT_FLOATS + 255) / 256;
+
+__global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict__ desc,
+                                                      const ObjState* __restrict__ st,
+                                                      const float* __restrict__ slots, float* __restrict__ red) {
+  const int o = blockIdx.x / SLOT_BLOCKS;
+  const ObjState& S = st[o];
+  if (S.status != ST_RUNNING || S.lite_viol > 0) return;
+  const int e = (blockIdx.x - o * SLOT_BLOCKS) * 256 + threadIdx.x;
+  if (e >= SLOT_FLOATS) return;
+  const float* s0 = slots + (size_t)desc[o].slot_sdf * SLOT_FLOATS + e;
+  auto sum = [&](int n) {
+    double x = 0.0;
+    int t = 0;
+    for (; t + 8 <= n; t += 8, s0 += 8 * SLOT_FLOATS) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = s0[u * SLOT_FLOATS];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x += (double)v[u];
+    }
+    for (; t < n; ++t, s0 += SLOT_FLOATS) x += (double)*s0;
+    return (float)x;
+  };
+  const float a = sum(S.n_sdf_tiles);
+  const float b = sum(S.n_ren_tiles);
+  red[(size_t)o * 2 * SLOT_FLOATS + e] = a;
+  red[(size_t)o * 2 * SLOT_FLOATS + SLOT_FLOATS + e] = b;
+}
+
 // trace_* hold [iteration][stride objects]; the pointers are pre-offset to this launch's
 // first object (object groups on concurrent streams, dsr_batch_run).
 __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDesc* __restrict__ desc,
                                                          ObjState* st, float* __restrict__ zbuf,
-                                                         GNParams P, const float* __restrict__ slots,
+                                                         GNParams P, const float* __restrict__ red,
                                                          float* __restrict__ trace_H,
                                                          float* __restrict__ trace_v,
                                                          int* __restrict__ trace_i, int stride) {
@@ -1384,45 +1455,15 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ int piv[NPAR];
   __shared__ float pivv[NPAR];
   __shared__ int flag;
-  const int ns = S.n_sdf_tiles, nk = S.n_ren_tiles;
 #ifdef DSR_SOLVE_PROFILE
   const long long tp0 = wall_clock64();
 #endif
-  {   // tile partials, fp64 combine in tile order; a thread's SPT elements load together
-    constexpr int SPT = (SLOT_FLOATS + SOLVE_THREADS - 1) / SOLVE_THREADS;
-    double a[SPT], b[SPT];
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) a[j] = b[j] = 0.0;
-    // (4 tiles' loads in flight per step: the partials were just written by the Jacobian
-    // kernel and come from L2/MALL, so a step is one memory latency)
-    const float* s0 = slots + (size_t)d.slot_sdf * SLOT_FLOATS + tid;
-    auto acc_tiles = [&](double (&x)[SPT], int n) {
-      int t = 0;
-      for (; t + 4 <= n; t += 4, s0 += 4 * SLOT_FLOATS) {
-        float v[4][SPT];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int j = 0; j < SPT; ++j)
-            v[u][j] = (tid + j * SOLVE_THREADS < SLOT_FLOATS) ? s0[u * SLOT_FLOATS + j * SOLVE_THREADS] : 0.f;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int j = 0; j < SPT; ++j) x[j] += (double)v[u][j];
-      }
-      for (; t < n; ++t, s0 += SLOT_FLOATS)
-#pragma unroll
-        for (int j = 0; j < SPT; ++j)
-          if (tid + j * SOLVE_THREADS < SLOT_FLOATS) x[j] += (double)s0[j * SOLVE_THREADS];
-    };
-    acc_tiles(a, ns);
-    acc_tiles(b, nk);
-#pragma unroll
-    for (int j = 0; j < SPT; ++j)
-      if (tid + j * SOLVE_THREADS < SLOT_FLOATS) {
-        Ss[tid + j * SOLVE_THREADS] = (float)a[j];
-        Sr[tid + j * SOLVE_THREADS] = (float)b[j];
-      }
+  {   // the tile partials' sums (k_reduce_slots)
+    const float* r = red + (size_t)o * 2 * SLOT_FLOATS;
+    for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {
+      Ss[e] = r[e];
+      Sr[e] = r[SLOT_FLOATS + e];
+    }
   }
   if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
   __syncthreads();

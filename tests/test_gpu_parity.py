@@ -556,7 +556,7 @@ def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
 
 @pytest.mark.gpu
 def test_refine_stops_at_ray_termination(gpu_decoder, monkeypatch):
-    """k_refine_compact skips band samples behind a ray's first certainly-full sample (their
+    """k_refine_scan skips band samples behind a ray's first certainly-full sample (their
     transmittance is exactly 0): results bitwise those of refining every band sample
     (DSR_REFINE_ALL=1), with fewer samples re-decoded."""
     import ctypes
