@@ -455,8 +455,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int n = 0; n < 512; ++n) {
     for (int i = 0; i < 3; ++i) w0x[n * 3 + i] = Wat(0, n, CODE + i);
     for (int k = 0; k < 64; ++k) {
-      w0z[n * 64 + k] = Wat(0, n, k);
-      w4z[n * 64 + k] = Wat(4, n, L3_OUT + k);
+      w0z[k * 512 + n] = Wat(0, n, k);          // k-major: the fold's loads coalesce over n
+      w4z[k * 512 + n] = Wat(4, n, L3_OUT + k);
     }
     w8[n] = Wat(8, 0, n);
   }
@@ -1185,8 +1185,8 @@ __global__ void k_fold_code(DevDecoder D, const float* __restrict__ z, float* __
   if (n >= HID) return;
   float s0 = 0.f, s4 = 0.f;
   for (int k = 0; k < CODE; ++k) {
-    s0 = __builtin_fmaf(D.W0z[n * CODE + k], z[k], s0);
-    s4 = __builtin_fmaf(D.W4z[n * CODE + k], z[k], s4);
+    s0 = __builtin_fmaf(D.W0z[k * HID + n], z[k], s0);
+    s4 = __builtin_fmaf(D.W4z[k * HID + n], z[k], s4);
   }
   bias0f[n] = D.bias[0][n] + s0;
   bias4f[n] = D.bias[4][n] + s4;

@@ -41,8 +41,8 @@ struct DevDecoder {
   int Kb[8];             // K of each backward GEMM (512; 448 for lin3^T)
   const float* bias[8];  // b_l padded to 512 (l = 0..7)
   const float* W0x;      // [512][3]  lin0 xyz columns
-  const float* W0z;      // [512][64] lin0 code columns (folded into a per-object bias)
-  const float* W4z;      // [512][64] lin4 code columns (folded into a per-object bias)
+  const float* W0z;      // [64][512] lin0 code columns, k-major (folded into a per-object bias)
+  const float* W4z;      // [64][512] lin4 code columns, k-major (folded into a per-object bias)
   const float* W8;       // [512]     lin8 row
   float b8;
   // split-fp16 copies of the forward A-fragments (dsr_mlp16.hpp):

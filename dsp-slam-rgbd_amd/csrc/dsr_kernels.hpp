@@ -213,8 +213,8 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
   for (int n = tid; n < HID; n += blockDim.x) {
     float s0 = 0.f, s4 = 0.f;
     for (int k = 0; k < CODE; ++k) {
-      s0 = __builtin_fmaf(D.W0z[n * CODE + k], z[k], s0);
-      s4 = __builtin_fmaf(D.W4z[n * CODE + k], z[k], s4);
+      s0 = __builtin_fmaf(D.W0z[k * HID + n], z[k], s0);
+      s4 = __builtin_fmaf(D.W4z[k * HID + n], z[k], s4);
     }
     bias0f[o * HID + n] = D.bias[0][n] + s0;
     bias4f[o * HID + n] = D.bias[4][n] + s4;
