@@ -139,7 +139,7 @@ def stats_sum(acc, st):
             acc[k] = max(acc.get(k, 0.0), v)
         elif k in ("lite_min_margin",):
             acc[k] = min(acc.get(k, 1e30), v)
-        elif k in ("lite", "keep_masks", "pad_"):
+        elif k in ("lite", "keep_masks", "surface_in_exact"):
             acc[k] = v
         else:
             acc[k] = acc.get(k, 0) + v
@@ -168,16 +168,22 @@ def kernel_rooflines(a):
     if a.get("lite"):
         entry("k_mlp_fwd_lite_st", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
               FP16_MFMA_PEAK_TF, FP16_MFMA_LOOP_TF, "2*1,769,984 per decoded ray sample, fp16 products")
-        entry("k_mlp_fwd16 (exact re-decode: band + audit)", 2.0 * FWD_MAC * a["refine_points"],
-              a["refine_ms"], a["refine_launches"], split_peak, split_loop,
-              "2*1,769,984 per re-decoded sample, fp32-equivalent (3xFP16)")
+        surf = a["jac_surface_points"] if a.get("surface_in_exact") else 0
+        entry("k_mlp_fwd16 (exact pass: band + audit samples" + (", surface points)" if surf else ")"),
+              2.0 * FWD_MAC * (a["refine_points"] + surf), a["refine_ms"], a["refine_launches"], split_peak,
+              split_loop, "2*1,769,984 per re-decoded sample" + (" and surface point" if surf else "")
+              + ", fp32-equivalent (3xFP16)")
     else:
         entry("k_mlp_fwd16", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
               split_peak, split_loop, "2*1,769,984 per decoded ray sample, fp32-equivalent (3xFP16)")
-    jflop = 2.0 * (FWD_MAC + BWD_MAC) * a["jac_surface_points"] + 2.0 * ren_mac * a["jac_render_points"]
-    entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop,
-          "N surface points x 2*(1,769,984+1,835,520) + K render points x 2*"
-          + ("1,835,520 (backward only, kept masks)" if a.get("keep_masks") else "(fwd+bwd)"))
+    if a.get("surface_in_exact"):      # every tile backward only (the exact pass ran the forwards)
+        jflop = 2.0 * BWD_MAC * (a["jac_surface_points"] + a["jac_render_points"])
+        note = "(N surface + K render points) x 2*1,835,520 (backward only, kept masks)"
+    else:
+        jflop = 2.0 * (FWD_MAC + BWD_MAC) * a["jac_surface_points"] + 2.0 * ren_mac * a["jac_render_points"]
+        note = ("N surface points x 2*(1,769,984+1,835,520) + K render points x 2*"
+                + ("1,835,520 (backward only, kept masks)" if a.get("keep_masks") else "(fwd+bwd)"))
+    entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop, note)
     return out
 
 

@@ -634,7 +634,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     pts_off += x.n_pts;
     ray_off += x.n_rays;
     cand_off += cap;
-    ftile_o[o] = (cap + TILE - 1) / TILE;
+    ftile_o[o] = (cap + TILE - 1) / TILE + (x.n_pts + TILE - 1) / TILE;   // + surface tiles (exact pass)
     jtile_o[o] = (x.n_pts + TILE - 1) / TILE + (cap + TILE - 1) / TILE;
     ftiles += ftile_o[o];
     slot_off += jtile_o[o];
@@ -683,11 +683,22 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   if (b->lite) {
     const char* km = getenv("DSR_KEEP_MASKS");
     if (!(km && atoi(km) == 0)) {     // 512 B of masks per sample of the worst case: HBM is ample
-      ALLOC(b->ma.msk, sizeof(uint16_t) * 256 * (size_t)std::max(1, cand_off));
-      ALLOC(b->ma.yv, sizeof(float) * (size_t)std::max(1, cand_off));
+      // slots: the samples' (cand order), then the surface points' (MaskArgs.surf_base)
+      ALLOC(b->ma.msk, sizeof(uint16_t) * 256 * ((size_t)cand_off + pts_off));
+      ALLOC(b->ma.yv, sizeof(float) * ((size_t)cand_off + pts_off));
       ALLOC(b->ma.slotmap, sizeof(int) * (size_t)std::max(1, cand_off));
       ALLOC(b->kslot, sizeof(int) * (size_t)std::max(1, cand_off));
       b->ma.kslot = b->kslot;
+      // the exact pass runs the surface points' forward too (MaskArgs.pts), so the Jacobian
+      // kernel chains only backward passes: bitwise the same results; it shortens small
+      // batches' chains (8-object Redwood keyframe -7%) and costs 64-object batches ~1%
+      // (the forward moves, the MFMA work is equal).  DSR_SURFACE_EXACT=0/1 overrides.
+      const char* se = getenv("DSR_SURFACE_EXACT");
+      const bool surf = se ? atoi(se) != 0 : n_obj <= 16;
+      if (surf && fwd_variant() == 12) {
+        b->ma.pts = b->pts;
+        b->ma.surf_base = cand_off;
+      }
     }
     ALLOC(b->refine, (size_t)std::max(1, cand_off));
     ALLOC(b->rbits, sizeof(uint64_t) * (size_t)std::max(1, ray_off));
@@ -940,7 +951,7 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
-                           b->lite ? LTILE : TILE);
+                           b->lite ? LTILE : TILE, 0);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
         if (b->lite)
@@ -958,7 +969,8 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
                            b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt);
         hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
                            b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
-        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
+                           (b->ma.pts && fv == 12) ? 1 : 0);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
         if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
@@ -1063,6 +1075,7 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->refine_launches = (b->timed && b->lite) ? used_iters * G : 0;
   st->lite = b->lite ? 1 : 0;
   st->keep_masks = (b->lite && b->ma.msk && fwd_variant() == 12) ? 1 : 0;
+  st->surface_in_exact = (st->keep_masks && b->ma.pts && jac_variant() == 12) ? 1 : 0;
   if (b->lite) {
     st->lite_min_margin = 1e30;
     for (const ObjState& o : hs) {

@@ -92,7 +92,8 @@ struct ObjState {
 };
 
 struct Tile {
-  int obj, term, start, count;   // term: 0 = sdf (surface points), 1 = render (K list)
+  int obj, term, start, count;   // term: 0 = sdf (surface points), 1 = render (K list),
+                                 // 3 = surface points in the exact pass (MaskArgs.pts)
 };
 
 // Early ray termination (k_sample_pass): the fwd kernels flag a ray dead once one of its
@@ -145,11 +146,17 @@ __device__ __forceinline__ float lite_perturb(const ErtArgs& E, float y, int idx
 //   msk[slot][layer 0..7][wave 0..7][g 0..3]: 16 bits = rows 64w + 16q + 4g + r (bit 4q+r)
 //   yv[slot]: sdf; slotmap[sample] = slot (or -1); kslot[k] = slot of render point k
 // (slot, sample and k are offsets from the object's cand_off)
+//   Surface points (pts != nullptr): the exact pass also runs the forward of every
+//   surface-point tile (Tile.term 3) and keeps its masks + sdf at slot
+//   surf_base + pts_off + point, so the Jacobian kernel runs the backward chain only for
+//   every tile, sdf and render alike (one weight direction per kernel: half the L2 set).
 struct MaskArgs {
   uint16_t* msk;
   float* yv;
   int* slotmap;
   const int* kslot;
+  const float* pts;      // surface points (camera frame), or nullptr: the Jacobian forwards them
+  int surf_base;         // first mask slot of the surface points
 };
 
 struct GNParams {
@@ -160,6 +167,15 @@ struct GNParams {
   float lite_floor;      // ... smallest margin
   float lite_safety;     // ... margin = max(floor, safety x max observed lite error)
 };
+
+// (p[...,None,:] * T[:3,:3]).sum(-1) + T[:3,3]   (loss.py:31-32, :74-77)
+__device__ __forceinline__ float3 xform(const float* T, float x, float y, float z) {
+  float3 o;
+  o.x = ((x * T[0] + y * T[1]) + z * T[2]) + T[3];
+  o.y = ((x * T[4] + y * T[5]) + z * T[6]) + T[7];
+  o.z = ((x * T[8] + y * T[9]) + z * T[10]) + T[11];
+  return o;
+}
 
 __device__ __forceinline__ float fetch4(const float4& v, int j) {
   return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));

@@ -161,14 +161,6 @@ __device__ void exp_se3_dev(const float* x, float* out) {
   }
 }
 
-// (p[...,None,:] * T[:3,:3]).sum(-1) + T[:3,3]   (loss.py:31-32, :74-77)
-__device__ __forceinline__ float3 xform(const float* T, float x, float y, float z) {
-  float3 o;
-  o.x = ((x * T[0] + y * T[1]) + z * T[2]) + T[3];
-  o.y = ((x * T[4] + y * T[5]) + z * T[6]) + T[7];
-  o.z = ((x * T[8] + y * T[9]) + z * T[10]) + T[11];
-  return o;
-}
 
 // ------------------------------------------------------------------------------------
 // state init / per-iteration prologue
@@ -582,18 +574,29 @@ __device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit 
   return carry;
 }
 
+// with_pts (exact pass, kept masks): each object's sample tiles, then its surface-point
+// tiles (term 3, the same 64-point groups as the Jacobian's sdf tiles)
 __global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize) {
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize, int with_pts) {
   const int total = tile_scan(
       n_obj, 0,
       [&](int o, int& n, int& nt) {
-        n = (st[o].status == ST_RUNNING) ? st[o].n_emit : 0;
+        const bool run = st[o].status == ST_RUNNING;
+        n = run ? st[o].n_emit : 0;
         nt = (n + tsize - 1) / tsize;
+        if (with_pts && run) nt += (desc[o].n_pts + TILE - 1) / TILE;
       },
       [&](int idx, int o, int i, int n) {
         Tile t;
-        t.obj = o; t.term = 0; t.start = i * tsize;
-        t.count = min(tsize, n - i * tsize);
+        const int nb = (n + tsize - 1) / tsize;
+        t.obj = o;
+        if (i < nb) {
+          t.term = 0; t.start = i * tsize;
+          t.count = min(tsize, n - i * tsize);
+        } else {
+          t.term = 3; t.start = (i - nb) * TILE;
+          t.count = min(TILE, desc[o].n_pts - t.start);
+        }
         tiles[idx] = t;
       });
   if (threadIdx.x == 0) *n_tiles = total;
@@ -1154,13 +1157,20 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     int sa;
     // render points whose ReLU masks and sdf the exact re-decode kept (MaskArgs): only the
     // backward chain runs; otherwise the forward recomputes them (loss.py:157)
+    // (sdf tiles: the exact pass ran their forward too, MaskArgs.pts)
     bool fast = false;
     if (MA.kslot != nullptr && tl.term == 1) {
       const int tid = opaque(threadIdx.x);
       int bad = 0;
       if (tid < tl.count) bad = MA.kslot[d.cand_off + tl.start + tid] < 0;
       fast = !__syncthreads_or(bad);
+    } else if (MA.pts != nullptr && tl.term == 0) {
+      fast = true;
     }
+    // absolute mask slot of the tile's point p
+    auto mslot = [&](int p) {
+      return tl.term == 1 ? d.cand_off + MA.kslot[d.cand_off + tl.start + p] : MA.surf_base + d.pts_off + tl.start + p;
+    };
     if (fast) {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
 #pragma unroll
@@ -1169,8 +1179,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       for (int cb = 0; cb < 4; ++cb) {
         const int p = 16 * cb + c;
         if (p < tl.count) {
-          const int slot = MA.kslot[d.cand_off + tl.start + p];
-          const uint16_t* src = MA.msk + (size_t)(d.cand_off + slot) * 256 + w * 4 + g;
+          const uint16_t* src = MA.msk + (size_t)mslot(p) * 256 + w * 4 + g;
 #pragma unroll
           for (int l = 0; l < 8; ++l) {
             const unsigned u = src[l * 32];
@@ -1180,8 +1189,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         }
       }
       const int tid = opaque(threadIdx.x);
-      if (tid < TILE)
-        sm.y[tid] = (tid < tl.count) ? MA.yv[d.cand_off + MA.kslot[d.cand_off + tl.start + tid]] : 0.f;
+      if (tid < TILE) sm.y[tid] = (tid < tl.count) ? MA.yv[mslot(tid)] : 0.f;
       __syncthreads();
     } else {
       // ---- lin0 (VALU, fp32) + masks

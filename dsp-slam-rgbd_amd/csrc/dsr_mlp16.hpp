@@ -434,10 +434,23 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
+    // term 3 (MSK): surface points, object frame as in the Jacobian kernel; their masks and
+    // sdf go to the surface slots, nothing else is written for them
+    const bool surf = MSK && tl.term == 3;
+    const int mbase = surf ? MA.surf_base + d.pts_off + tl.start : d.cand_off + tl.start;
     {
       const int tid = opaque(threadIdx.x);
       if (tid < TILE) {
-        const float4 v = (tid < tl.count) ? cand[d.cand_off + tl.start + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tid < tl.count) {
+          if (surf) {
+            const float* p = MA.pts + (size_t)(d.pts_off + tl.start + tid) * 3;
+            const float3 xo = xform(E.st[tl.obj].T, p[0], p[1], p[2]);
+            v = make_float4(xo.x, xo.y, xo.z, 0.f);
+          } else {
+            v = cand[d.cand_off + tl.start + tid];
+          }
+        }
         *reinterpret_cast<float4*>(sm.xyz + tid * 4) = v;
       }
     }
@@ -469,7 +482,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       }
       sa = block_scale(m, sm.wmax, w, lane);
       write_split(v, sa, sm.Hh, sm.Hl, w, lane);
-      if constexpr (MSK) store_mask16(relu_bits(v), MA.msk, d.cand_off + tl.start, tl.count, 0, w, lane);
+      if constexpr (MSK) store_mask16(relu_bits(v), MA.msk, mbase, tl.count, 0, w, lane);
     }
     __syncthreads();
     floatx4 acc[4][4];
@@ -479,7 +492,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
       uint64_t mk;
       sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
-      if constexpr (MSK) store_mask16(mk, MA.msk, d.cand_off + tl.start, tl.count, l, w, lane);
+      if constexpr (MSK) store_mask16(mk, MA.msk, mbase, tl.count, l, w, lane);
       __syncthreads();
     }
     {
@@ -494,7 +507,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
       uint64_t mask;
       epi_l7(acc, D, sm.red, w, lane, mask);
-      if constexpr (MSK) store_mask16(mask, MA.msk, d.cand_off + tl.start, tl.count, 7, w, lane);
+      if constexpr (MSK) store_mask16(mask, MA.msk, mbase, tl.count, 7, w, lane);
     }
     __syncthreads();
     {
@@ -508,21 +521,25 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
         const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
         if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) y = __builtin_nanf("");
-        const int tagged = __float_as_int(p.w);
-        const int idx = tagged & ~AUDIT_BIT;
-        if (E.st) {                        // re-decode after the lite pass: track the lite error
-          const float yl = dense[d.cand_off + idx];
-          const float e = fabsf(y - yl);
-          if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
-          if (tagged & AUDIT_BIT) {        // audited out-of-band sample: same class exactly?
-            const int cl = yl <= E.nth ? 0 : (yl < -E.nth ? 1 : 2);   // full | band | empty
-            const int ce = y <= E.nth ? 0 : (y < -E.nth ? 1 : 2);
-            if (cl != ce) atomicAdd(&E.st[tl.obj].lite_viol, 1);
+        if (surf) {
+          MA.yv[mbase + tid] = y;
+        } else {
+          const int tagged = __float_as_int(p.w);
+          const int idx = tagged & ~AUDIT_BIT;
+          if (E.st) {                      // re-decode after the lite pass: track the lite error
+            const float yl = dense[d.cand_off + idx];
+            const float e = fabsf(y - yl);
+            if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+            if (tagged & AUDIT_BIT) {      // audited out-of-band sample: same class exactly?
+              const int cl = yl <= E.nth ? 0 : (yl < -E.nth ? 1 : 2);   // full | band | empty
+              const int ce = y <= E.nth ? 0 : (y < -E.nth ? 1 : 2);
+              if (cl != ce) atomicAdd(&E.st[tl.obj].lite_viol, 1);
+            }
           }
+          dense[d.cand_off + idx] = y;
+          if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
+          if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
         }
-        dense[d.cand_off + idx] = y;
-        if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
-        if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
       }
     }
     __syncthreads();

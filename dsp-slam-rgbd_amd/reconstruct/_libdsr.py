@@ -79,7 +79,7 @@ class Stats(C.Structure):
                 ("lite_min_margin", C.c_double), ("jac_surface_points", C.c_int64),
                 ("jac_render_points", C.c_int64), ("keep_masks", C.c_int),
                 ("lite_audit_violations", C.c_int), ("lite_redo_objects", C.c_int),
-                ("pad_", C.c_int), ("audit_points", C.c_int64)]
+                ("surface_in_exact", C.c_int), ("audit_points", C.c_int64)]
 
 
 #: every function declared in include/dsr.h, with its ctypes signature

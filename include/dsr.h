@@ -139,7 +139,8 @@ typedef struct {
                                      band / empty) differed from the lite pass's */
   int lite_redo_objects;          /* objects that discarded an iteration for a violation and
                                      finished with exact decoding */
-  int pad_;
+  int surface_in_exact;           /* 1: the exact pass ran the surface points' forward too and
+                                     the Jacobian kernel only backward chains (kept masks) */
   int64_t audit_points;           /* out-of-band samples re-decoded exactly as an audit */
 } dsr_stats;
 
