@@ -671,3 +671,36 @@ def test_large_batch_tile_tables(gpu_decoder, monkeypatch):
         assert batch[i]["loss"] == single[0]["loss"], i
         for key in ("H", "b", "n_valid", "k"):
             assert np.array_equal(tr[i][key], tr1[0][key]), (i, key)
+
+
+@pytest.mark.gpu
+def test_surface_forward_in_exact_pass_bitwise(gpu_decoder, monkeypatch):
+    """Small batches run the surface points' forward in the exact pass and keep their ReLU
+    masks (MaskArgs.pts), so the Jacobian kernel only chains backward passes; the forward
+    is the same split-fp16 arithmetic on the same 64-point tiles, so every output and count
+    is bitwise that of the Jacobian kernel forwarding them itself (DSR_SURFACE_EXACT=0)."""
+    import ctypes
+
+    import bench
+    from reconstruct import _libdsr as L
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    monkeypatch.setenv("DSR_LITE", "1")
+    sig = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DSR_SURFACE_EXACT", mode)
+        h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 6, 1000)
+        try:
+            outs = (L.ObjectOut * 6)()
+            ctx.check(lib.dsr_batch_run(h), "run")
+            ctx.check(lib.dsr_batch_download(h, outs), "download")
+            st = L.Stats()
+            ctx.check(lib.dsr_batch_stats(h, ctypes.byref(st)), "stats")
+            rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
+                           np.float32)
+            sig[mode] = (rec, st.fwd_points, st.refine_points, st.jac_surface_points, st.jac_render_points)
+            assert st.surface_in_exact == int(mode)
+        finally:
+            lib.dsr_batch_destroy(h)
+    assert np.array_equal(sig["0"][0].view(np.uint32), sig["1"][0].view(np.uint32))
+    assert sig["0"][1:] == sig["1"][1:]
