@@ -641,11 +641,12 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   }
   {
     // object groups on concurrent streams: 2 for large batches (the decoder
-    // grids fill the chip; more groups only overlap their launches), 4 for small ones (a
-    // strong-scaled shard of 8-16 objects is bound by its latency kernels, which the extra
-    // groups hide: 8 objects 280 -> 301 obj/s)
+    // grids fill the chip; more groups only overlap their launches), 4 for small batches of
+    // large objects (a strong-scaled shard of 8-16 KITTI objects is bound by its latency
+    // kernels, which the extra groups hide: 8 objects 317 -> 333 obj/s), 2 again for small
+    // batches of small objects (8 Redwood keyframe hypotheses: 5.31 -> 5.16 ms)
     const char* e = getenv("DSR_STREAMS");
-    int G = e ? atoi(e) : (n_obj <= 16 ? 4 : 2);
+    int G = e ? atoi(e) : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
     G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
     if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
     for (int g = 0; g < G; ++g) {
