@@ -6,7 +6,8 @@ Tolerances:
 * one teacher-forced GN iteration vs golden F4 (same state in): N_valid and K within
   2 (samples within fp32 rounding of |x| = 1 or |sdf| = th flip between any two fp32
   implementations; the loss bound grows by the most one flipped render point can move
-  it), loss rel <= 1e-5 at identical K, H <= 2e-3, b and dx <= 5e-2 max-normalised and
+  it), loss rel <= 1e-5 at identical K, H and b (all but b[3:6]) <= 5e-4 at identical K
+  (<= 2e-3 / 5e-3 with a flipped render point), b[3:6] and dx <= 5e-2 max-normalised and
   the step <= 1e-2 in the H-norm (b[3:6] carries k4 * J_rot * r_rot with k4 = 1e7 and
   r_rot an fp32 cancellation quantised in 6e-8 steps, in the reference itself);
 * full trajectories: mask flips (|sdf|=th, de_do=1e-2, |x|=1) and ReLU kinks at the
@@ -118,12 +119,25 @@ def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
             # by ~1e-7 absolute (numpy fp32 vs fp64: rms 7.6e-8, tools/diag_precision.py),
             # so mean(r^2) carries ~2e-5 relative noise in every fp32 implementation
             assert abs(t["sdf_loss"][0] - f["it_sdf_loss"][e]) <= 5e-5 * f["it_sdf_loss"][e]
-        assert rel(t["H"][0], f["it_H"][e]) <= 2e-3, e
+        eh = rel(t["H"][0], f["it_H"][e])
         # b[3:6] carries k4 * J_rot * r_rot with k4 = 1e7 and r_rot = 1 - cos(tilt), an fp32
-        # cancellation in the reference itself: max-norm loose, step in the H-norm tight
-        assert rel(t["b"][0], f["it_b"][e]) <= 5e-2, e
-        assert step_err(t["dx"][0], f["it_dx"][e], f["it_H"][e]) <= 1e-2, e
-        assert rel(t["dx"][0], f["it_dx"][e]) <= 5e-2, e
+        # cancellation in the reference itself (quantised in 6e-8 steps): those three entries
+        # are held loosely, the other 68 like H; dx in the H-norm (the step GN takes)
+        rest = np.r_[0:3, 6:71]
+        eb = rel(np.asarray(t["b"][0])[rest], np.asarray(f["it_b"][e])[rest])
+        eb_rot = rel(t["b"][0], f["it_b"][e])
+        es = step_err(t["dx"][0], f["it_dx"][e], f["it_H"][e])
+        edx = rel(t["dx"][0], f["it_dx"][e])
+        print(f"{name} it {e}: dK {dk} H {eh:.2e} b {eb:.2e} b(all) {eb_rot:.2e} dx(H-norm) {es:.2e} dx {edx:.2e}")
+        # measured (r2, every F4 state): identical K -> H <= 1.2e-4, b <= 1.4e-4; one flipped
+        # render point -> H <= 2.4e-4, b <= 1.5e-3; b with the prior entries <= 1.3e-2,
+        # dx <= 9.9e-3 in the H-norm and 1.7e-2 max-normalised (both at kitti5 it 9, whose
+        # b[3:6] cancellation is the largest)
+        assert eh <= (5e-4 if dk == 0 else 2e-3), (e, eh)
+        assert eb <= (5e-4 if dk == 0 else 5e-3), (e, eb)
+        assert eb_rot <= 5e-2, e
+        assert es <= 1e-2, e
+        assert edx <= 5e-2, e
 
 
 @pytest.mark.parametrize("name,optim,dtype", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),
