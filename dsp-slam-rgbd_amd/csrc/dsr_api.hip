@@ -964,10 +964,9 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
       }
       if (b->lite) {                             // exact split-fp16 decode of the band samples
-        if (b->ma.slotmap)
-          DSR_CHECK(ctx, hipMemsetAsync(b->ma.slotmap + gr.c0, 0xff, sizeof(int) * (size_t)(gr.c1 - gr.c0), s));
         hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->M,
-                           b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt);
+                           b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt,
+                           b->ma.slotmap);
         hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
                            b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
@@ -996,10 +995,9 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
                          (const float4*)nullptr, (float*)nullptr, (float*)nullptr,
                          keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
-      hipLaunchKernelGGL(k_count, dim3((ng + 63) / 64), dim3(64), 0, s, ng, desc, st, it,
-                         b->counts + (size_t)o0 * NCOUNT, n);
       float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
-      hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred);
+      hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred, it,
+                         b->counts + (size_t)o0 * NCOUNT, n);
       hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, sred,
                          b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
                          b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,

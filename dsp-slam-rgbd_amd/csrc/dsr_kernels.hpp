@@ -429,7 +429,8 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
                                                              int M, unsigned char* __restrict__ refine,
                                                              const float* __restrict__ dense, float nth,
                                                              uint64_t* __restrict__ rbits_g,
-                                                             uint64_t* __restrict__ abits_g, int* __restrict__ ccnt) {
+                                                             uint64_t* __restrict__ abits_g, int* __restrict__ ccnt,
+                                                             int* __restrict__ slotmap) {
   const RenderChunk ch = chunks[blockIdx.x];
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
@@ -465,7 +466,10 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
         const int stop = __builtin_ctzll(ub);
         b = fb & (((1ull << stop) - 1) | (tb & (1ull << stop)));
       }
-      if (rr < d.n_rays && lane < M) refine[d.cand_off + (size_t)rr * M + lane] = 0;
+      if (rr < d.n_rays && lane < M) {
+        refine[d.cand_off + (size_t)rr * M + lane] = 0;
+        if (slotmap) slotmap[d.cand_off + (size_t)rr * M + lane] = -1;   // k_refine_emit sets the refined
+      }
       if (lane == i0 + u) {
         rbits[tid] = b;
         abits[tid] = b & ab;
@@ -1399,13 +1403,31 @@ constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render,
 // and SLOT_BLOCKS workgroups per object, 8 tiles' loads in flight per thread — the same
 // sums, in the same order, as one workgroup walking the tiles, without that walk's ~90
 // dependent memory latencies per object.  red[o][0][e] = sdf sums, red[o][1][e] = render.
+// The first workgroup of each object also records the iteration's work counts
+// (counts[it][o][NCOUNT], dsr_batch_stats) before k_solve may end the object.
 constexpr int SLOT_BLOCKS = (SLOT_FLOATS + 255) / 256;
+constexpr int NCOUNT = 6;
 
 __global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict__ desc,
                                                       const ObjState* __restrict__ st,
-                                                      const float* __restrict__ slots, float* __restrict__ red) {
+                                                      const float* __restrict__ slots, float* __restrict__ red,
+                                                      int it, int* __restrict__ counts, int stride) {
   const int o = blockIdx.x / SLOT_BLOCKS;
   const ObjState& S = st[o];
+  if (blockIdx.x == o * SLOT_BLOCKS && threadIdx.x == 0) {
+    int* c = counts + ((size_t)it * stride + o) * NCOUNT;
+    if (S.status != ST_RUNNING) {               // finished / failed objects did no work
+      for (int i = 0; i < NCOUNT; ++i) c[i] = 0;
+    } else {
+      const bool jac = S.n_ren_tiles > 0 || S.k > 0;
+      c[0] = S.n_eval;
+      c[1] = jac ? desc[o].n_pts + S.k : 0;
+      c[2] = S.n_valid;
+      c[3] = S.n_refine;
+      c[4] = S.n_audit;
+      c[5] = jac ? S.k : 0;                     // render points of c[1] (the rest: surface)
+    }
+  }
   if (S.status != ST_RUNNING || S.lite_viol > 0) return;
   const int e = (blockIdx.x - o * SLOT_BLOCKS) * 256 + threadIdx.x;
   if (e >= SLOT_FLOATS) return;
@@ -1744,26 +1766,6 @@ __global__ void k_inv_out(int n_obj, const ObjState* __restrict__ st, float* __r
 
 // per-iteration counters for the algorithmic-FLOP bookkeeping:
 // decoded samples, Jacobian points (N + K), in-ball samples, exact re-decodes, audits, K
-constexpr int NCOUNT = 6;
-__global__ void k_count(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                        int it, int* __restrict__ counts, int stride) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= n_obj) return;
-  const ObjState& S = st[o];
-  int* c = counts + ((size_t)it * stride + o) * NCOUNT;
-  if (S.status != ST_RUNNING) {                 // finished / failed objects did no work
-    for (int i = 0; i < NCOUNT; ++i) c[i] = 0;
-    return;
-  }
-  const bool jac = S.n_ren_tiles > 0 || S.k > 0;
-  c[0] = S.n_eval;
-  c[1] = jac ? desc[o].n_pts + S.k : 0;
-  c[2] = S.n_valid;
-  c[3] = S.n_refine;
-  c[4] = S.n_audit;
-  c[5] = jac ? S.k : 0;                         // render points of c[1] (the rest: surface)
-}
-
 __global__ void k_finalize(int n_obj, const ObjState* __restrict__ st, const float* __restrict__ zbuf,
                            dsr_object_out* __restrict__ out) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;

@@ -718,3 +718,33 @@ def test_surface_forward_in_exact_pass_bitwise(gpu_decoder, monkeypatch):
             lib.dsr_batch_destroy(h)
     assert np.array_equal(sig["0"][0].view(np.uint32), sig["1"][0].view(np.uint32))
     assert sig["0"][1:] == sig["1"][1:]
+
+
+@pytest.mark.gpu
+def test_ray_chunk_boundaries_vs_oracle(gpu_decoder, oracle_dec):
+    """The render and refine kernels run one workgroup per 128 rays of an object (ray
+    chunks) and stitch the chunks' ordered outputs together: objects whose
+    ray counts sit on and around chunk boundaries (128, 129, 256, 257, 383 rays), batched
+    together, each give the oracle's first GN step from the same state."""
+    from oracle import dsr_oracle as O
+
+    opt = _opt(gpu_decoder, dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
+                                                                     num_iterations=1)), "Redwood")
+    shapes = [(100, 28), (100, 29), (200, 56), (200, 57), (300, 83)]
+    obs = [S.make_object(900 + i, n_pts=n, n_bg=b, scale=1.0, tz=3.0, upright=False)
+           for i, (n, b) in enumerate(shapes)]
+    assert [o.rays.shape[0] for o in obs] == [128, 129, 256, 257, 383]
+    res, tr = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in obs], trace=True)
+    P = O.OptimParams.from_cfg(S.REDWOOD_OPTIM)
+    for i, o in enumerate(obs):
+        assert res[i]["is_good"], (i, res[i])
+        t = tr[i]
+        n_fg = o.depth.shape[0]
+        dobs = np.concatenate([o.depth, np.zeros(o.rays.shape[0] - n_fg)]).astype(np.float32)
+        tro, _, _ = O.gn_step(oracle_dec, P, t["t_obj_cam"][0], t["z"][0], o.pts, o.rays, dobs, n_fg)
+        dk = abs(int(t["k"][0]) - tro.k)
+        assert dk <= 2 and abs(int(t["n_valid"][0]) - tro.n_valid) <= 2, i
+        assert abs(t["sdf_loss"][0] - tro.sdf_loss) <= 5e-5 * abs(tro.sdf_loss), i
+        assert abs(t["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
+                                                              + max(dk, 2) * 0.09 / tro.k), i
+        assert rel(t["H"][0], tro.H) <= 5e-3, i
