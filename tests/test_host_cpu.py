@@ -127,3 +127,29 @@ def test_grid_decode_order_matches_reference_f9(oracle_dec):
     d = int(f["dim"])
     vol = O.decode_sdf(oracle_dec, f["code"], create_voxel_grid(vol_dim=d)).reshape(d, d, d)
     assert np.abs(vol - f["volume"]).max() <= 2e-5
+
+
+@pytest.mark.parametrize("change,what", [
+    ({"weight_norm": False}, "LayerNorm"),
+    ({"xyz_in_all": True}, "xyz_in_all"),
+    ({"use_tanh": True}, "use_tanh"),
+    ({"latent_in": [3]}, "latent_in"),
+])
+def test_unsupported_decoder_variants_rejected_loudly(change, what):
+    """decoder variants libdsr does not implement (deep_sdf_decoder.py:46-47,
+    58-67, 89-102) are refused before anything reaches the device, never approximated."""
+    import copy
+
+    import synthetic as S
+    from deep_sdf.workspace import check_topology, fold_state
+
+    layers = fold_state(S.make_decoder(1234), S.DEFAULT_SPECS)
+    check_topology(S.DEFAULT_SPECS, layers)                  # the supported topology passes
+    specs = copy.deepcopy(S.DEFAULT_SPECS)
+    specs["NetworkSpecs"].update(change)
+    with pytest.raises(NotImplementedError, match=what):
+        check_topology(specs, layers)
+    specs = copy.deepcopy(S.DEFAULT_SPECS)
+    specs["CodeLength"] = 32
+    with pytest.raises(NotImplementedError, match="CodeLength"):
+        check_topology(specs, layers)
