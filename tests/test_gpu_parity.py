@@ -748,3 +748,32 @@ def test_ray_chunk_boundaries_vs_oracle(gpu_decoder, oracle_dec):
         assert abs(t["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
                                                               + max(dk, 2) * 0.09 / tro.k), i
         assert rel(t["H"][0], tro.H) <= 5e-3, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [17, 32, 64])
+def test_depth_sample_counts_vs_oracle(gpu_decoder, oracle_dec, m):
+    """num_depth_samples (configs' `num_depth_samples`, optimizer.py:126) other than 50:
+    odd, small, and the largest supported (64: every lane of the refine scan, the largest
+    render LDS rows) — the first GN step of a small batch vs the oracle's."""
+    from oracle import dsr_oracle as O
+
+    optim = dict(S.REDWOOD_OPTIM, num_depth_samples=m,
+                 joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"], num_iterations=1))
+    opt = _opt(gpu_decoder, optim, "Redwood")
+    obs = [S.redwood_object(60 + i, n_pts=300) for i in range(3)]
+    res, tr = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in obs], trace=True)
+    P = O.OptimParams.from_cfg(optim)
+    assert P.num_depth_samples == m
+    for i, o in enumerate(obs):
+        assert res[i]["is_good"], (i, res[i])
+        t = tr[i]
+        n_fg = o.depth.shape[0]
+        dobs = np.concatenate([o.depth, np.zeros(o.rays.shape[0] - n_fg)]).astype(np.float32)
+        tro, _, _ = O.gn_step(oracle_dec, P, t["t_obj_cam"][0], t["z"][0], o.pts, o.rays, dobs, n_fg)
+        dk = abs(int(t["k"][0]) - tro.k)
+        assert dk <= 2 and abs(int(t["n_valid"][0]) - tro.n_valid) <= 2, (m, i)
+        assert abs(t["sdf_loss"][0] - tro.sdf_loss) <= 5e-5 * abs(tro.sdf_loss), (m, i)
+        assert abs(t["render_loss"][0] - tro.render_loss) <= (1e-5 * abs(tro.render_loss)
+                                                              + max(dk, 2) * 0.09 / tro.k), (m, i)
+        assert rel(t["H"][0], tro.H) <= 5e-3, (m, i)
