@@ -474,6 +474,18 @@ __device__ __forceinline__ void st_wait(int* c, int target, int* broken) {
   asm volatile("" ::: "memory");
 }
 
+#ifdef DSR_EXP_STAMP   // diagnostic build (tools: exp_STAMP.so): per-wave cycles by phase, block 0-3
+#define LSTAMP(cat)                                                         \
+  {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
+    stamp[cat] += t_ - stamp_last;                                          \
+    stamp_last = t_;                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+  }
+#else
+#define LSTAMP(cat)
+#endif
 template <bool PRIO, int LV>
 __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Tile* __restrict__ tiles,
                                                          const int* __restrict__ n_tiles,
@@ -512,12 +524,17 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           half8, __builtin_amdgcn_raw_buffer_load_b128(r1, lane * 16, q * (D.Kf[1] / 32) * WS * 1024, 0));
   }
   __syncthreads();                       // the only block-wide barrier
+#ifdef DSR_EXP_STAMP
+  unsigned long long stamp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   int it = 0;
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x, ++it) {
     const int p = it & 1;
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
     float* xyz = sm.xyz[grp];
+    LSTAMP(7)
     // ---- tile inputs, per group
     {
       const int lane = opaque(threadIdx.x & 63);
@@ -534,6 +551,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       st_signal(&sm.cT[grp]);
       st_wait(&sm.cT[grp], 4 * (it + 1), &sm.broken);
     }
+    LSTAMP(0)
     floatx4 acc[4][8];
     // ---- lin0 (3 inputs, fp32 VALU) into the accumulator layout
     {
@@ -563,9 +581,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         }
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
+      LSTAMP(1)
       st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * 7 * it, &sm.broken);   // readers of lin7's input
+      LSTAMP(2)
       lite_write<(LV & 1024) != 0>(acc, 0, sm.H, w, lane);
       st_signal(&sm.cH[grp]);
+      LSTAMP(3)
     }
     // ---- lin1..lin7 (lin7: + relu, lin8 dot product -> red)
     auto gemm = [&](int l) {
@@ -576,8 +597,19 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         st_wait(&sm.cH[1], hs, &sm.broken);
         if (lag > 0) st_wait(&sm.cP, 4 * ng, &sm.broken);
       }
+      LSTAMP(4)
       auto hook = [&](int t) {
+#ifdef DSR_EXP_STAMP
+        if (t == 7 && grp == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          const unsigned long long h0 = __builtin_amdgcn_s_memtime();
+          st_wait(&sm.cH[1], hs, &sm.broken);
+          stamp[8] += __builtin_amdgcn_s_memtime() - h0;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#else
         if (t == 7 && grp == 0) st_wait(&sm.cH[1], hs, &sm.broken);
+#endif
         if (t == 8) st_signal(&sm.cRlo);
         if (t == lag && grp == 0) st_signal(&sm.cP);
       };
@@ -591,6 +623,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       lite_gemm_x<PRIO, LV>(WA[l], D.Kf[l] / 32, WA[ln], D.Kf[ln] / 32, w, sm.H, acc, ring,
                             opaque(threadIdx.x & 63), hook, ci);
       st_signal(&sm.cRhi);
+      LSTAMP(5)
     };
 #pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
@@ -626,7 +659,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           }
         }
         if (!(__int_as_float(mi) < 32768.f)) sm.ovf[p] = it + 1;
+        LSTAMP(6)
         st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
+        LSTAMP(2)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -638,6 +673,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
                                         4 * lite_swz_g(g, c, (LV & 1024) != 0)) = hv[q][cb];
           }
         st_signal(&sm.cH[grp]);
+        LSTAMP(3)
         continue;
       }
       const float usc = ldexpf(1.f, -D.sw[l]);
@@ -731,6 +767,13 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       st_signal(&sm.cE);
     }
   }
+#ifdef DSR_EXP_STAMP
+  LSTAMP(7)
+  if (blockIdx.x < 4 && (threadIdx.x == 0 || threadIdx.x == 256))
+    printf("lite_stamp %d %d %d %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", (int)blockIdx.x, w, it,
+           stamp[0], stamp[1], stamp[2], stamp[3], stamp[4], stamp[5], stamp[6], stamp[7], stamp[8]);
+#endif
 }
+#undef LSTAMP
 
 }  // namespace dsr
