@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,7 +32,15 @@ struct dsr_ctx {
   hipStream_t stream = nullptr;
   hipStream_t gstream[MAX_GROUPS] = {};   // [0] = stream; [1..] object-group streams
   std::string err;
+  // Device memory and events of destroyed batches, reused by the next ones: a keyframe
+  // stream, or the per-call reconstruct_object API, creates one batch per call, and
+  // hipMalloc / hipFree (which synchronises) / hipEventCreate cost more than a small
+  // batch's GN run takes.  Capped at POOL_CAP bytes; released by dsr_ctx_destroy.
+  std::multimap<size_t, void*> pool;      // free device blocks by size
+  size_t pool_bytes = 0;
+  std::vector<hipEvent_t> ev_timing, ev_plain;
 };
+static constexpr size_t POOL_CAP = (size_t)16 << 30;
 
 // Forward-kernel variant (DSR_FWD_VARIANT: bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
 // bit3 split-fp16; 12 = split-fp16 + setprio, the default) and the A-ring depth of the split
@@ -160,7 +169,7 @@ struct dsr_batch {
   int M = 50;
   std::vector<ObjDesc> hdesc;
   int cand_total = 0, slot_total = 0, fwd_tile_cap = 0, jac_tile_cap = 0;
-  std::vector<void*> allocs;
+  std::vector<std::pair<void*, size_t>> allocs;   // (block, its size): back to the context pool
   // device
   ObjDesc* desc = nullptr;
   ObjState* st = nullptr;
@@ -272,6 +281,9 @@ int dsr_ctx_create(int device, dsr_ctx** out) {
 int dsr_ctx_destroy(dsr_ctx* ctx) {
   if (!ctx) return 0;
   hipSetDevice(ctx->device);
+  for (auto& kv : ctx->pool) hipFree(kv.second);
+  for (hipEvent_t e : ctx->ev_timing) hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev_plain) hipEventDestroy(e);
   for (int g = 1; g < MAX_GROUPS; ++g)
     if (ctx->gstream[g]) hipStreamDestroy(ctx->gstream[g]);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -538,11 +550,31 @@ static std::vector<int> render_passes(int M, long samples) {
 }
 static size_t ev_per_iter(const dsr_batch* b) { return 2 * (b->passes.size() - 1 + (b->lite ? 1 : 0)) + 2; }
 
+// A batch buffer: the smallest pooled block that fits (and wastes at most half of itself
+// plus 1 MB), else hipMalloc.
 static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
-  if (bytes == 0) bytes = 256;
-  if (hipMalloc(p, bytes) != hipSuccess) return fail(b->ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
-  b->allocs.push_back(*p);
+  dsr_ctx* ctx = b->ctx;
+  bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
+  auto it = ctx->pool.lower_bound(bytes);
+  if (it != ctx->pool.end() && it->first <= 2 * bytes + ((size_t)1 << 20)) {
+    *p = it->second;
+    b->allocs.emplace_back(it->second, it->first);
+    ctx->pool_bytes -= it->first;
+    ctx->pool.erase(it);
+    return 0;
+  }
+  if (hipMalloc(p, bytes) != hipSuccess) return fail(ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
+  b->allocs.emplace_back(*p, bytes);
   return 0;
+}
+static hipError_t pool_event(dsr_ctx* ctx, hipEvent_t* e, bool timing) {
+  auto& v = timing ? ctx->ev_timing : ctx->ev_plain;
+  if (!v.empty()) {
+    *e = v.back();
+    v.pop_back();
+    return hipSuccess;
+  }
+  return timing ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
 }
 
 // Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
@@ -579,13 +611,25 @@ static GNParams make_params(const dsr_optim_params* p) {
 
 int dsr_batch_destroy(dsr_batch* b) {
   if (!b) return 0;
-  hipSetDevice(b->ctx->device);
-  for (auto& e : b->ev) hipEventDestroy(e);
+  dsr_ctx* ctx = b->ctx;
+  hipSetDevice(ctx->device);
+  // the blocks go back to the pool: no kernel of this batch may still be using them
+  for (size_t g = 0; g < std::max<size_t>(1, b->groups.size()); ++g) hipStreamSynchronize(ctx->gstream[g]);
   if (b->graph) hipGraphExecDestroy(b->graph);
-  for (auto& e : b->join_ev) hipEventDestroy(e);
-  if (b->fork_ev) hipEventDestroy(b->fork_ev);
-  if (b->done_ev) hipEventDestroy(b->done_ev);
-  for (void* p : b->allocs) hipFree(p);
+  for (auto& e : b->ev)
+    if (e) ctx->ev_timing.push_back(e);
+  for (hipEvent_t e : b->join_ev)
+    if (e) ctx->ev_plain.push_back(e);
+  if (b->fork_ev) ctx->ev_plain.push_back(b->fork_ev);
+  if (b->done_ev) ctx->ev_plain.push_back(b->done_ev);
+  for (auto& a : b->allocs) {
+    if (ctx->pool_bytes + a.second <= POOL_CAP) {
+      ctx->pool.emplace(a.second, a.first);
+      ctx->pool_bytes += a.second;
+    } else {
+      hipFree(a.first);
+    }
+  }
   delete b;
   return 0;
 }
@@ -704,7 +748,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ALLOC(b->refine, (size_t)std::max(1, cand_off));
     ALLOC(b->rbits, sizeof(uint64_t) * (size_t)std::max(1, ray_off));
     ALLOC(b->abits, sizeof(uint64_t) * (size_t)std::max(1, ray_off));
-    if (hipMemset(b->refine, 0, (size_t)std::max(1, cand_off)) != hipSuccess) {
+    if (hipMemsetAsync(b->refine, 0, (size_t)std::max(1, cand_off), ctx->stream) != hipSuccess) {
       dsr_batch_destroy(b);
       return fail(ctx, "hipMemset failed");
     }
@@ -764,25 +808,18 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     return fail(ctx, "hipMemcpy (inputs) failed");
   }
   if (trace) {
-    hipMemset(b->tr_H, 0, sizeof(float) * NPAR * NPAR * std::max(1, b->iters) * n_obj);
-    hipMemset(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj);
-    hipMemset(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj);
+    hipMemsetAsync(b->tr_H, 0, sizeof(float) * NPAR * NPAR * std::max(1, b->iters) * n_obj, ctx->stream);
+    hipMemsetAsync(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj, ctx->stream);
+    hipMemsetAsync(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj, ctx->stream);
   }
   b->passes = render_passes(M, (long)cand_off);
   b->ev.resize((size_t)std::max(1, b->loop_iters) * b->groups.size() * ev_per_iter(b) + 2);
   b->join_ev.resize(b->groups.size());
   for (auto& e : b->ev)
-    if (hipEventCreate(&e) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
+    if (pool_event(ctx, &e, true) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
   for (auto& e : b->join_ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      dsr_batch_destroy(b);
-      return fail(ctx, "hipEventCreate failed");
-    }
-  if (hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming) != hipSuccess) {
-    dsr_batch_destroy(b);
-    return fail(ctx, "hipEventCreate failed");
-  }
-  if (hipEventCreateWithFlags(&b->fork_ev, hipEventDisableTiming) != hipSuccess) {
+    if (pool_event(ctx, &e, false) != hipSuccess) { dsr_batch_destroy(b); return fail(ctx, "hipEventCreate failed"); }
+  if (pool_event(ctx, &b->done_ev, false) != hipSuccess || pool_event(ctx, &b->fork_ev, false) != hipSuccess) {
     dsr_batch_destroy(b);
     return fail(ctx, "hipEventCreate failed");
   }
