@@ -195,3 +195,28 @@ def test_mesher_grid_decode_vs_reference_f9(gpu_decoder):
     assert np.array_equal(mex.voxel_points, f["grid"])
     vol = mex.decode_grid(f["code"]).reshape(d, d, d)
     assert np.abs(vol - f["volume"]).max() <= 2e-5
+
+
+def test_pooled_batch_memory_reuse_bitwise(gpu_decoder, full_layers):
+    """A context hands destroyed batches' device blocks and events to the next batches
+    (dsr_api.hip: batch_alloc / pool_event).  Reused blocks hold the previous batch's
+    values, so every buffer a run reads must be written first: results after a different
+    batch ran in the same context equal those of a fresh context, bitwise."""
+    from deep_sdf.workspace import Decoder
+    from reconstruct import _libdsr as L
+
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=3)
+    big = [S.make_object(800 + i, n_pts=400 + 37 * i, n_bg=150, scale=1.0, tz=3.0, upright=False)
+           for i in range(6)]
+    small = [S.make_object(850 + i, n_pts=200 + 11 * i, n_bg=60, scale=1.0, tz=3.0, upright=False)
+             for i in range(3)]
+    for _ in range(2):                    # the context now holds both batches' blocks in its pool
+        opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in big])
+    reused = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in small])
+    fresh_dec = Decoder(S.DEFAULT_SPECS, full_layers, ctx=L.Context(0))
+    fresh = _opt(fresh_dec, S.REDWOOD_OPTIM, "Redwood", iters=3).reconstruct_objects(
+        [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in small])
+    for a, b in zip(reused, fresh):
+        assert a["is_good"] == b["is_good"] and a["loss"] == b["loss"]
+        if a["is_good"]:
+            assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"]) and np.array_equal(a["code"], b["code"])
