@@ -241,8 +241,10 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         floatx4 x = decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb];
+#ifndef DSR_EXP_ONEPROD            // timing experiment (invalid results): the hi.hi product only
         x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[j][q], bh[cb & 1], x, 0, 0, 0);
         x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bl[cb & 1], x, 0, 0, 0);
+#endif
         acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bh[cb & 1], x, 0, 0, 0);
       }
     }
