@@ -1312,17 +1312,15 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       const float usc = ldexpf(1.f, -(D.swb[l] + sa));
       float m = 0.f;
       const uint64_t mask = mk[l - 1];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float a = accr(acc[q][cb], r) * usc;    // exact (power of two)
-            const float gv = ((mask >> ((q * 4 + cb) * 4 + r)) & 1ull) ? a : 0.f;
-            v[q][cb][r] = gv;
-            m = fmaxf(m, fabsf(gv));
-          }
+      // element (q, cb, r) = bit (q * 4 + cb) * 4 + r of the mask: compile-time indices
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        ([&] {
+          constexpr int q = K >> 4, cb = (K >> 2) & 3, r = K & 3;
+          const float gv = keep_if<K>(accr(acc[q][cb], r) * usc, mask);   // exact (power of two)
+          v[q][cb][r] = gv;
+          m = fmaxf(m, fabsf(gv));
+        }(), ...);
+      }(std::make_integer_sequence<int, 64>{});
       if (l == 4 && w >= 6) {
         // d/d[code, xyz] via the latent skip: lin3^T's input rows n >= 445 are lin4's code and
         // xyz columns (wave 7: rows 448..511 all; wave 6: rows 445..447 = q 3, g 3, r 1..3).

@@ -324,8 +324,15 @@ __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _F
       for (int r = 0; r < 4; r += 2) {
         const float2v x = float2v{v[q][cb][r], v[q][cb][r + 1]} * sc2;
         const half2v h = __builtin_convertvector(x, half2v);
-        const half2v l = __builtin_convertvector(x - __builtin_convertvector(h, float2v), half2v);
         hh[r] = h[0]; hh[r + 1] = h[1];
+        // lo = fp16(x - h): x - h is exact in fp32, so one fma_mix (f16 operand -h, f32 x,
+        // rounded once to f16) per value equals fp16(x - fp32(h)) without the two back-
+        // conversions and the subtraction
+        const unsigned hb = __builtin_bit_cast(unsigned, h);
+        unsigned lb;
+        asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lb) : "v"(hb), "v"(x[0]));
+        asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lb) : "v"(hb), "v"(x[1]));
+        const half2v l = __builtin_bit_cast(half2v, lb);
         hl[r] = l[0]; hl[r + 1] = l[1];
       }
       *reinterpret_cast<half4*>(Hh + p * PH + n0) = hh;
@@ -349,6 +356,17 @@ __device__ __forceinline__ void store_mask16(uint64_t mk, uint16_t* msk, int can
     for (int q = 0; q < 4; ++q) u |= (unsigned)((mk >> (16 * q + 4 * cb)) & 0xFull) << (4 * q);
     if (p < count) msk[(size_t)(cand_base + p) * 256 + l * 32 + w * 4 + g] = (uint16_t)u;
   }
+}
+
+// a if bit I of mask is set, else +0.0: v_bfe_i32 (the bit sign-extended to a 0 / all-ones
+// word) + v_and_b32 — bitwise the select `bit ? a : 0.f`, which the compiler otherwise emits
+// as and + compare + cndmask (the bit extract is asm so it is not folded back into that)
+template <int I>
+__device__ __forceinline__ float keep_if(float a, uint64_t mask) {
+  const unsigned word = (unsigned)(mask >> (I & 32));
+  int m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(word), "i"(I & 31));
+  return __int_as_float(__float_as_int(a) & m);
 }
 
 __device__ __forceinline__ uint64_t relu_bits(const float (&v)[4][4][4]) {
