@@ -1,0 +1,22 @@
+"""Per-phase cycle shares of k_mlp_jac16 from an exp_STAMP.so run.
+
+Usage: python tools/jac_stamp_summary.py gpurun_out/stamp.txt
+(lines `jac_stamp block wave tiles c0..c7` printed by blocks 0-3, waves 0 and 4)
+"""
+import sys
+
+import numpy as np
+
+NAMES = ["tile inputs / kept masks", "GEMMs", "epilogue compute", "scale exchange (barrier)",
+         "split writes", "post-write barrier", "J tail", "other (lin0, g7, lin7, lin0^T)"]
+rows = [ln.split()[1:] for ln in open(sys.argv[1]) if ln.startswith("jac_stamp")]
+a = np.array(rows, dtype=np.float64)
+for w in (0, 4):
+    sel = a[a[:, 1] == w]
+    if not len(sel):
+        continue
+    tot = sel[:, 3:11].sum()
+    print(f"wave {w}: {len(sel)} block-launches, {sel[:, 2].sum():.0f} tiles, "
+          f"{tot / max(1, sel[:, 2].sum()):.0f} cycles per tile")
+    for n, v in zip(NAMES, sel[:, 3:11].sum(0) / tot):
+        print(f"   {n:34s} {v:.3f}")
