@@ -1218,11 +1218,12 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int p = 16 * cb + c;
-        if (p < tl.count) {
-          const uint16_t* src = MA.msk + (size_t)mslot(p) * 256 + w * 4 + g;
+        if (p < tl.count) {   // layers 0..7 of this lane's slice: one 16-byte load (mask_store)
+          const uint4 m4 = *reinterpret_cast<const uint4*>(MA.msk + (size_t)mslot(p) * 256 + (w * 4 + g) * 8);
+          const unsigned dw[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
           for (int l = 0; l < 8; ++l) {
-            const unsigned u = src[l * 32];
+            const unsigned u = (dw[l >> 1] >> (16 * (l & 1))) & 0xFFFFu;
 #pragma unroll
             for (int q = 0; q < 4; ++q) mk[l] |= (uint64_t)((u >> (4 * q)) & 0xFu) << (16 * q + 4 * cb);
           }

@@ -344,17 +344,37 @@ __device__ __forceinline__ void write_split(const float (&v)[4][4][4], int s, _F
 // Shared epilogue: v = relu(acc * 2^-unscale + bias) (+ xyz rows for lin3), block max,
 // one barrier, scale, split-write.  Returns the new activation scale exponent.
 // 16-bit lane slices of a layer's ReLU mask (bit (q*4+cb)*4+r of mk, the Jacobian kernel's
-// layout) for the lane's 4 points, stored per sample as MaskArgs.msk
-__device__ __forceinline__ void store_mask16(uint64_t mk, uint16_t* msk, int cand_base, int count, int l,
-                                             int w, int lane) {
+// layout) for the lane's 4 points, kept per sample as MaskArgs.msk [point][w][g][layer] (256
+// uint16 per point): a lane's 8 layers of one point are 16 contiguous bytes, so the exact
+// pass stores them once per tile and the Jacobian kernel loads them with one 16-byte load.
+// MaskQueue collects them layer by layer in registers (each push shifts the 8-slot queue by
+// one uint16: after layers 0..7, dword k holds layers 2k | 2k+1).
+struct MaskQueue {
+  unsigned d[4][4];            // [cb][dword]
+};
+
+__device__ __forceinline__ void mask_push(MaskQueue& mq, uint64_t mk) {
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    unsigned u = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u |= (unsigned)((mk >> (16 * q + 4 * cb)) & 0xFull) << (4 * q);
+    mq.d[cb][0] = (mq.d[cb][0] >> 16) | (mq.d[cb][1] << 16);
+    mq.d[cb][1] = (mq.d[cb][1] >> 16) | (mq.d[cb][2] << 16);
+    mq.d[cb][2] = (mq.d[cb][2] >> 16) | (mq.d[cb][3] << 16);
+    mq.d[cb][3] = (mq.d[cb][3] >> 16) | (u << 16);
+  }
+}
+
+__device__ __forceinline__ void mask_store(const MaskQueue& mq, uint16_t* msk, int cand_base, int count, int w,
+                                           int lane) {
   const int g = lane >> 4, c = lane & 15;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
     const int p = 16 * cb + c;
-    unsigned u = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) u |= (unsigned)((mk >> (16 * q + 4 * cb)) & 0xFull) << (4 * q);
-    if (p < count) msk[(size_t)(cand_base + p) * 256 + l * 32 + w * 4 + g] = (uint16_t)u;
+    if (p < count)
+      *reinterpret_cast<uint4*>(msk + (size_t)(cand_base + p) * 256 + (w * 4 + g) * 8) =
+          make_uint4(mq.d[cb][0], mq.d[cb][1], mq.d[cb][2], mq.d[cb][3]);
   }
 }
 
@@ -477,6 +497,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     __syncthreads();
     // ---- lin0 on VALU (fp32), then split
     int sa;
+    MaskQueue mq;
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       const float* bias0 = bias0f + tl.obj * HID;
@@ -502,7 +523,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       }
       sa = block_scale(m, sm.wmax, w, lane);
       write_split(v, sa, sm.Hh, sm.Hl, w, lane);
-      if constexpr (MSK) store_mask16(relu_bits(v), MA.msk, mbase, tl.count, 0, w, lane);
+      if constexpr (MSK) mask_push(mq, relu_bits(v));
     }
     __syncthreads();
     floatx4 acc[4][4];
@@ -512,7 +533,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
       uint64_t mk;
       sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
-      if constexpr (MSK) store_mask16(mk, MA.msk, mbase, tl.count, l, w, lane);
+      if constexpr (MSK) mask_push(mq, mk);
       __syncthreads();
     }
     {
@@ -527,7 +548,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
       uint64_t mask;
       epi_l7(acc, D, sm.red, w, lane, mask);
-      if constexpr (MSK) store_mask16(mask, MA.msk, mbase, tl.count, 7, w, lane);
+      if constexpr (MSK) {
+        mask_push(mq, mask);
+        mask_store(mq, MA.msk, mbase, tl.count, w, lane);
+      }
     }
     __syncthreads();
     {
