@@ -1168,10 +1168,12 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #ifdef DSR_EXP_STAMP
     ++jtiles;
 #endif
+    float zpre = 0.f;   // the code's NaN probe for the tail, loaded now (wave 0)
     {
       const int tid = opaque(threadIdx.x);
       if (tid < TILE) {
         float x = 0.f, y = 0.f, z = 0.f, aux = 0.f, rr = 0.f;
+        zpre = bias0f[tl.obj * HID];
         if (tid < tl.count) {
           if (tl.term == 0) {
             const float* p = pts_all + (size_t)(d.pts_off + tl.start + tid) * 3;
@@ -1426,7 +1428,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     const int tid = opaque(threadIdx.x);
     if (tid < TILE) {
       const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
-      const float zprobe = bias0f[tl.obj * HID];
+      const float zprobe = zpre;
       if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) {
         sm.y[tid] = __builtin_nanf("");
         for (int e = 0; e < IN; ++e) sm.gin[tid * GIN_PITCH + e] = __builtin_nanf("");

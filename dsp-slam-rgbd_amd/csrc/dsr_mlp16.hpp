@@ -418,8 +418,15 @@ __device__ __forceinline__ void xyz_rows(float (&v)[4][NCB][4], const float* xyz
   }
 }
 
+struct NoStamp {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// `stamp(phase)` marks phase ends for the DSR_EXP_STAMP diagnostic build (k_mlp_fwd16)
+template <class Stamp = NoStamp>
 __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
-                                     Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk) {
+                                     Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk,
+                                     Stamp stamp = Stamp{}) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
@@ -443,6 +450,7 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
     }
   }
   if (is_l3 && w == 6) xyz_rows(v, sm.xyz, lane, m);
+  stamp(2);
   m = wave_max(m, lane);
   if (lane == 0) sm.wmax[w] = m;
   __syncthreads();                       // all waves done reading H; maxima published
@@ -450,7 +458,9 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
 #pragma unroll
   for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
   const int s = act_scale_exp(mm);
+  stamp(3);
   write_split(v, s, sm.Hh, sm.Hl, w, lane);
+  stamp(4);
   mk = bits;
   return s;
 }
@@ -471,17 +481,39 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   const int nt = *n_tiles;
   constexpr bool MSK = (X & 512) != 0;
   constexpr int NB = ((X >> 10) & 3) == 0 ? 0 : 1 + ((X >> 10) & 3);
+#ifdef DSR_EXP_STAMP   // diagnostic build: per-wave cycles by phase (as k_mlp_jac16's JSTAMP)
+  unsigned long long fst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long fst_last = __builtin_amdgcn_s_memtime();
+  int ftiles = 0;
+  auto stamp = [&](int cat) {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    fst[cat] += t - fst_last;
+    fst_last = t;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#else
+  NoStamp stamp;
+#endif
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x) {
+#ifdef DSR_EXP_STAMP
+    ++ftiles;
+#endif
     const Tile tl = tiles[ti];
     const ObjDesc d = desc[tl.obj];
     // term 3 (MSK): surface points, object frame as in the Jacobian kernel; their masks and
     // sdf go to the surface slots, nothing else is written for them
     const bool surf = MSK && tl.term == 3;
     const int mbase = surf ? MA.surf_base + d.pts_off + tl.start : d.cand_off + tl.start;
+    // wave 0 (point tid = lane) also fetches what the tile's tail reads from global memory —
+    // the code's NaN probe and the sample's lite value — so those loads are in flight
+    // during the layers instead of exposed in the tail, where the other waves wait for it
+    float zpre = 0.f, ylpre = 0.f;
     {
       const int tid = opaque(threadIdx.x);
       if (tid < TILE) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        zpre = bias0f[tl.obj * HID];
         if (tid < tl.count) {
           if (surf) {
             const float* p = MA.pts + (size_t)(d.pts_off + tl.start + tid) * 3;
@@ -489,12 +521,14 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
             v = make_float4(xo.x, xo.y, xo.z, 0.f);
           } else {
             v = cand[d.cand_off + tl.start + tid];
+            if (E.st) ylpre = dense[d.cand_off + (__float_as_int(v.w) & ~AUDIT_BIT)];
           }
         }
         *reinterpret_cast<float4*>(sm.xyz + tid * 4) = v;
       }
     }
     __syncthreads();
+    stamp(0);
     // ---- lin0 on VALU (fp32), then split
     int sa;
     MaskQueue mq;
@@ -530,15 +564,21 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
 #pragma unroll 1
     for (int l = 1; l <= 6; ++l) {
       const int lane = opaque(threadIdx.x & 63);
+      stamp(7);
       gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
+      stamp(1);
       uint64_t mk;
-      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk);
+      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, stamp);
       if constexpr (MSK) mask_push(mq, mk);
+      stamp(7);
       __syncthreads();
+      stamp(5);
     }
     {
       const int lane = opaque(threadIdx.x & 63);
+      stamp(7);
       gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane);
+      stamp(1);
       const int un = D.sw[7] + sa;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -556,6 +596,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     __syncthreads();
     {
       const int tid = opaque(threadIdx.x);
+      float emax = 0.f;
       if (tid < tl.count) {
         float s = sm.red[tid];
         for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
@@ -563,7 +604,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
         // enter through the point or the code, so re-impose it here
         const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
-        const float zprobe = bias0f[tl.obj * HID];     // NaN iff the code holds a NaN
+        const float zprobe = zpre;                     // NaN iff the code holds a NaN
         if (p.x != p.x || p.y != p.y || p.z != p.z || zprobe != zprobe) y = __builtin_nanf("");
         if (surf) {
           MA.yv[mbase + tid] = y;
@@ -571,9 +612,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           const int tagged = __float_as_int(p.w);
           const int idx = tagged & ~AUDIT_BIT;
           if (E.st) {                      // re-decode after the lite pass: track the lite error
-            const float yl = dense[d.cand_off + idx];
+            const float yl = ylpre;
             const float e = fabsf(y - yl);
-            if (e == e) atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(e));
+            if (e == e) emax = e;
             if (tagged & AUDIT_BIT) {      // audited out-of-band sample: same class exactly?
               const int cl = yl <= E.nth ? 0 : (yl < -E.nth ? 1 : 2);   // full | band | empty
               const int ce = y <= E.nth ? 0 : (y < -E.nth ? 1 : 2);
@@ -585,9 +626,21 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
         }
       }
+      // the tile's largest |lite - exact|: one atomic per tile instead of one per sample
+      if (w == 0 && E.st && !surf) {
+        emax = wave_max(emax, opaque(threadIdx.x & 63));
+        if ((threadIdx.x & 63) == 0 && emax > 0.f)
+          atomicMax(reinterpret_cast<int*>(&E.st[tl.obj].lite_err), __float_as_int(emax));
+      }
     }
     __syncthreads();
+    stamp(6);
   }
+#ifdef DSR_EXP_STAMP
+  if (blockIdx.x < 4 && (threadIdx.x == 0 || threadIdx.x == 256))
+    printf("fwd16_stamp %d %d %d %llu %llu %llu %llu %llu %llu %llu %llu\n", (int)blockIdx.x, w, ftiles, fst[0],
+           fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7]);
+#endif
 }
 
 }  // namespace dsr

@@ -1,7 +1,8 @@
 """Per-phase cycle shares of k_mlp_jac16 from an exp_STAMP.so run.
 
-Usage: python tools/jac_stamp_summary.py gpurun_out/stamp.txt
-(lines `jac_stamp block wave tiles c0..c7` printed by blocks 0-3, waves 0 and 4)
+Usage: python tools/jac_stamp_summary.py gpurun_out/stamp.txt [jac_stamp|fwd16_stamp]
+(lines `jac_stamp|fwd16_stamp block wave tiles c0..c7` printed by blocks 0-3, waves 0 and 4;
+fwd16: phase 6 = tanh + outputs, 7 = lin0 + mask queue, 0 = tile inputs)
 """
 import sys
 
@@ -9,7 +10,8 @@ import numpy as np
 
 NAMES = ["tile inputs / kept masks", "GEMMs", "epilogue compute", "scale exchange (barrier)",
          "split writes", "post-write barrier", "J tail", "other (lin0, g7, lin7, lin0^T)"]
-rows = [ln.split()[1:] for ln in open(sys.argv[1]) if ln.startswith("jac_stamp")]
+KEY = sys.argv[2] if len(sys.argv) > 2 else "jac_stamp"
+rows = [ln.split()[1:] for ln in open(sys.argv[1]) if ln.startswith(KEY + " ")]
 a = np.array(rows, dtype=np.float64)
 for w in (0, 4):
     sel = a[a[:, 1] == w]
