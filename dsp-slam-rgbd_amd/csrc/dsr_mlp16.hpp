@@ -482,7 +482,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   constexpr bool MSK = (X & 512) != 0;
   constexpr int NB = ((X >> 10) & 3) == 0 ? 0 : 1 + ((X >> 10) & 3);
 #ifdef DSR_EXP_STAMP   // diagnostic build: per-wave cycles by phase (as k_mlp_jac16's JSTAMP)
-  unsigned long long fst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long fst[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long fst_last = __builtin_amdgcn_s_memtime();
   int ftiles = 0;
   auto stamp = [&](int cat) {
@@ -592,8 +592,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         mask_push(mq, mask);
         mask_store(mq, MA.msk, mbase, tl.count, w, lane);
       }
+      stamp(8);
     }
     __syncthreads();
+    stamp(9);
     {
       const int tid = opaque(threadIdx.x);
       float emax = 0.f;
@@ -601,6 +603,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         float s = sm.red[tid];
         for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
         float y = tanhf(s + D.b8);
+        stamp(10);
         // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
         // enter through the point or the code, so re-impose it here
         const float4 p = *reinterpret_cast<const float4*>(sm.xyz + tid * 4);
@@ -626,6 +629,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
         }
       }
+      stamp(11);
       // the tile's largest |lite - exact|: one atomic per tile instead of one per sample
       if (w == 0 && E.st && !surf) {
         emax = wave_max(emax, opaque(threadIdx.x & 63));
@@ -638,8 +642,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   }
 #ifdef DSR_EXP_STAMP
   if (blockIdx.x < 4 && (threadIdx.x == 0 || threadIdx.x == 256))
-    printf("fwd16_stamp %d %d %d %llu %llu %llu %llu %llu %llu %llu %llu\n", (int)blockIdx.x, w, ftiles, fst[0],
-           fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7]);
+    printf("fwd16_stamp %d %d %d %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", (int)blockIdx.x, w,
+           ftiles, fst[0], fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7], fst[8], fst[9], fst[10], fst[11]);
 #endif
 }
 
