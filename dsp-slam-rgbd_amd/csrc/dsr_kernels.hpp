@@ -760,12 +760,28 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   if (tid < M) dep_s[tid] = S.depths[tid];
   const int nr = min(RENDER_RAYS, d.n_rays - ch.ray0);
   {
+    // element e -> (row e / M, column e % M) advanced without per-element divisions; four
+    // loads in flight per thread before their LDS stores
     const float* src = dense + d.cand_off + (size_t)ch.ray0 * M;
-    for (int e = tid; e < nr * M; e += RENDER_RAYS) {
-      const int r = e / M, j = e - r * M;
-      const float v = src[e];
-      T_s[r * pitch + j] = v;
-      D_s[r * pitch + j] = v;
+    const int tot = nr * M, sq = RENDER_RAYS / M, sr = RENDER_RAYS - sq * M;
+    int r = tid / M, j = tid - r * M;
+    for (int e = tid; e < tot; e += 4 * RENDER_RAYS) {
+      float v[4];
+      int o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = (e + u * RENDER_RAYS < tot) ? src[e + u * RENDER_RAYS] : 0.f;
+        o[u] = r * pitch + j;
+        j += sr;
+        r += sq;
+        if (j >= M) { j -= M; ++r; }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e + u * RENDER_RAYS < tot) {
+          T_s[o[u]] = v[u];
+          D_s[o[u]] = v[u];
+        }
     }
   }
   __syncthreads();
