@@ -35,49 +35,82 @@ namespace dsr {
 // small fp32 linear algebra (single thread), mirroring torch CPU fp32 semantics
 // ------------------------------------------------------------------------------------
 // LU with partial pivoting (first max, LAPACK getrf), multipliers by reciprocal (sgetf2).
+// Fully unrolled with the row swap as selects, so every index is static and the matrix stays
+// in registers (a swap through a run-time pivot index would put it in scratch memory).
 template <int N>
-__device__ void lu_small(float (&a)[N][N], int (&piv)[N]) {
+__device__ __forceinline__ void lu_small(float (&a)[N][N], int (&piv)[N]) {
+#pragma unroll
   for (int k = 0; k < N; ++k) {
     int p = k;
     float best = fabsf(a[k][k]);
+#pragma unroll
     for (int r = k + 1; r < N; ++r)
       if (fabsf(a[r][k]) > best) { best = fabsf(a[r][k]); p = r; }
     piv[k] = p;
-    if (p != k)
-      for (int c = 0; c < N; ++c) { float t = a[k][c]; a[k][c] = a[p][c]; a[p][c] = t; }
+#pragma unroll
+    for (int r = k + 1; r < N; ++r) {
+      const bool sw = (p == r);
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        const float t = a[k][c];
+        a[k][c] = sw ? a[r][c] : t;
+        a[r][c] = sw ? t : a[r][c];
+      }
+    }
     const float rc = 1.0f / a[k][k];
+#pragma unroll
     for (int r = k + 1; r < N; ++r) a[r][k] = a[r][k] * rc;
+#pragma unroll
     for (int r = k + 1; r < N; ++r)
+#pragma unroll
       for (int c = k + 1; c < N; ++c) a[r][c] = __builtin_fmaf(-a[r][k], a[k][c], a[r][c]);
   }
 }
 
 template <int N>
-__device__ void inv_small(const float* m, float* out) {   // torch.inverse (getrf + getrs(I))
+__device__ __forceinline__ void inv_small(const float* m, float* out) {   // torch.inverse (getrf + getrs(I))
   float a[N][N];
   int piv[N];
+#pragma unroll
   for (int i = 0; i < N; ++i)
+#pragma unroll
     for (int j = 0; j < N; ++j) a[i][j] = m[i * N + j];
   lu_small<N>(a, piv);
+#pragma unroll
   for (int col = 0; col < N; ++col) {
     float x[N];
+#pragma unroll
     for (int i = 0; i < N; ++i) x[i] = (i == col) ? 1.f : 0.f;
-    for (int k = 0; k < N; ++k)
-      if (piv[k] != k) { float t = x[k]; x[k] = x[piv[k]]; x[piv[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < N; ++k)       // row interchanges, as selects (static indices)
+#pragma unroll
+      for (int r = k + 1; r < N; ++r) {
+        const bool sw = (piv[k] == r);
+        const float t = x[k];
+        x[k] = sw ? x[r] : t;
+        x[r] = sw ? t : x[r];
+      }
+#pragma unroll
     for (int i = 0; i < N; ++i)
+#pragma unroll
       for (int l = 0; l < i; ++l) x[i] = __builtin_fmaf(-a[i][l], x[l], x[i]);
+#pragma unroll
     for (int i = N - 1; i >= 0; --i) {
+#pragma unroll
       for (int l = i + 1; l < N; ++l) x[i] = __builtin_fmaf(-a[i][l], x[l], x[i]);
       x[i] = x[i] / a[i][i];
     }
+#pragma unroll
     for (int i = 0; i < N; ++i) out[i * N + col] = x[i];
   }
 }
 
-__device__ float det3(const float* m4 /*4x4, uses [:3,:3]*/) {   // torch.det via LU
+__device__ __forceinline__ float det3(const float* m4 /*4x4, uses [:3,:3]*/) {   // torch.det via LU
   float a[3][3];
   int piv[3];
+#pragma unroll
   for (int i = 0; i < 3; ++i)
+#pragma unroll
     for (int j = 0; j < 3; ++j) a[i][j] = m4[i * 4 + j];
   lu_small<3>(a, piv);
   float d = (a[0][0] * a[1][1]) * a[2][2];
@@ -191,7 +224,7 @@ __global__ void k_init_state(int n_obj, const float* __restrict__ t_in, const in
 }
 
 // optimizer.py:122-128 and the code fold of lin0 / lin4.
-__global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
+__global__ __launch_bounds__(512) void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
                              const float* __restrict__ zbuf, DevDecoder D, GNParams P,
                              float* __restrict__ bias0f, float* __restrict__ bias4f,
                              float* __restrict__ dobs) {
@@ -212,10 +245,13 @@ __global__ void k_iter_begin(int n_obj, const ObjDesc* __restrict__ desc, ObjSta
     bias4f[o * HID + n] = D.bias[4][n] + s4;
   }
   if (tid == 0) {
-    inv_small<4>(S.T, S.Tco);                                  // :122
-    const float scale = powf(det3(S.Tco), 0.33333334f);        // :123 det ** (1/3)
-    const float dmin = S.Tco[11] - 1.0f * scale;               // :124
-    const float dmax = S.Tco[11] + 1.0f * scale;
+    float tco[16];                                             // (registers; S.Tco written once)
+    inv_small<4>(S.T, tco);                                    // :122
+#pragma unroll
+    for (int i = 0; i < 16; ++i) S.Tco[i] = tco[i];
+    const float scale = powf(det3(tco), 0.33333334f);          // :123 det ** (1/3)
+    const float dmin = tco[11] - 1.0f * scale;                 // :124
+    const float dmax = tco[11] + 1.0f * scale;
     const int M = P.M;
     const float step = (dmax - dmin) / (float)(M - 1);         // torch.linspace (CPU, fp32)
     const int half = M / 2;
@@ -1720,14 +1756,26 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // accumulates in the column-solve order)
   for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) X[e / NPAR][e % NPAR] = 0.f;
   __syncthreads();
-  if (tid == 0) {
-    int perm[NPAR];                       // P applied to the row indices of I
-    for (int i = 0; i < NPAR; ++i) perm[i] = i;
+  if (tid < 64) {
+    // P applied to the row indices of I: the pivots' swaps in order on a permutation held
+    // across wave 0 (lane i: perm[i] and perm[64 + i]) with lane reads / selects — a private
+    // array indexed by the run-time pivot would live in scratch memory, one dependent
+    // round trip per swap
+    static_assert(NPAR <= 128, "permutation held in two registers per lane");
+    const int lane = tid;
+    int pa = lane, pb = 64 + lane;
+    const int qa = piv[lane], qb = (64 + lane < NPAR) ? piv[64 + lane] : 0;
     for (int k = 0; k < NPAR; ++k) {
-      const int p = piv[k];
-      if (p != k) { const int t = perm[k]; perm[k] = perm[p]; perm[p] = t; }
+      const int p = (k < 64) ? __builtin_amdgcn_readlane(qa, k) : __builtin_amdgcn_readlane(qb, k - 64);
+      if (p != k) {
+        const int vk = (k < 64) ? __builtin_amdgcn_readlane(pa, k) : __builtin_amdgcn_readlane(pb, k - 64);
+        const int vp = (p < 64) ? __builtin_amdgcn_readlane(pa, p) : __builtin_amdgcn_readlane(pb, p - 64);
+        if (k < 64) pa = (lane == k) ? vp : pa; else pb = (lane == k - 64) ? vp : pb;
+        if (p < 64) pa = (lane == p) ? vk : pa; else pb = (lane == p - 64) ? vk : pb;
+      }
     }
-    for (int i = 0; i < NPAR; ++i) X[i][perm[i]] = 1.f;
+    X[lane][pa] = 1.f;
+    if (64 + lane < NPAR) X[64 + lane][pb] = 1.f;
   }
   __syncthreads();
   // Column c is solved by the 4 lanes 4c..4c+3 of one wave, lane `sub` holding rows
