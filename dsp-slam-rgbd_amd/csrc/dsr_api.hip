@@ -531,11 +531,13 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // boundaries, DSR_RENDER_PASSES="8,12,16,20,24,32" style (ascending, each < M); one pass
 // [0, M) when empty ("0" disables termination).  Default: fine windows for large batches
 // (fewer wasted samples), coarse ones for small batches whose passes are too short to
-// fill the chip (measured: 64 KITTI objects 186 vs 176 obj/s, 8 Redwood objects 10.6 vs
-// 11.2 ms per batch).
+// fill the chip: each pass costs at least one tile's latency, extra samples are nearly free
+// (measured: 64 KITTI objects 186 vs 176 obj/s, 8 Redwood objects 10.6 vs 11.2 ms per
+// batch; round 2, same box: 8 KITTI objects 341-346 obj/s with 16,24 vs 337-341 with
+// 8,16,24, keyframe batch 4.82 vs 4.98 ms).
 static std::vector<int> render_passes(int M, long samples) {
   const char* e = getenv("DSR_RENDER_PASSES");
-  std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : "8,16,24");
+  std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : "16,24");
   std::vector<int> r{0};
   size_t p = 0;
   while (p < spec.size()) {
