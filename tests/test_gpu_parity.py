@@ -406,7 +406,8 @@ def test_early_ray_termination_matches_full_decode(gpu_decoder, monkeypatch):
     objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
             for e in range(n_it)]
     out = {}
-    for spec in ("0", "8,12,16,20,24,32", "4,5,6,7,8,9,10,11,12,14,16,20,24,28,32,40"):
+    # (the large-batch default, the small-batch default, a fine schedule)
+    for spec in ("0", "8,12,16,20,24,32", "16,24", "4,5,6,7,8,9,10,11,12,14,16,20,24,28,32,40"):
         monkeypatch.setenv("DSR_RENDER_PASSES", spec)
         out[spec] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
     full_res, full_tr = out["0"]
