@@ -1248,7 +1248,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     uint64_t mk[8];
     float v[4][4][4];
     floatx4 acc[4][4];
-    int sa;
+    int sa;          // backward gradients: one scale per tile and layer
+    Scales2 fs;      // forward activations: per-group scales (block_scale2), as the exact pass
     // render points whose ReLU masks and sdf the exact re-decode kept (MaskArgs): only the
     // backward chain runs; otherwise the forward recomputes them (loss.py:157)
     // (sdf tiles: the exact pass ran their forward too, MaskArgs.pts)
@@ -1316,9 +1317,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           }
         }
         JSTAMP(7)
-        sa = block_scale(m, sm.wmax, w, lane);
+        fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
-        write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+        write_split(v, fs.of(w), sm.Hh, sm.Hl, w, lane);
         JSTAMP(4)
       }
       __syncthreads();
@@ -1327,9 +1328,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll 1
       for (int l = 1; l <= 6; ++l) {
         const int lane = opaque(threadIdx.x & 63), g = lane >> 4;
-        gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
+        gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
         JSTAMP(1)
-        const float usc = ldexpf(1.f, -(D.sw[l] + sa));
+        const float usc = ldexpf(1.f, -(D.sw[l] + fs.b));
         const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
         float m = 0.f;
         uint64_t bits = 0;
@@ -1350,9 +1351,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         mk[l] = bits;
         if (l == 3 && w == 6) xyz_rows(v, sm.xyz, lane, m);     // lin4 input = h3 | xyz
         JSTAMP(2)
-        sa = block_scale(m, sm.wmax, w, lane);
+        fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
-        write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+        write_split(v, fs.of(w), sm.Hh, sm.Hl, w, lane);
         JSTAMP(4)
         __syncthreads();
         JSTAMP(5)
@@ -1360,9 +1361,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       // ---- lin7 + lin8 dot + tanh
       {
         const int lane = opaque(threadIdx.x & 63);
-        gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane);
+        gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
         JSTAMP(1)
-        const int un = D.sw[7] + sa;
+        const int un = D.sw[7] + fs.b;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll

@@ -143,9 +143,20 @@ __device__ __forceinline__ void gemm16_tile_x(const half8* __restrict__ A, int T
 
 // EX: timing experiments only (invalid results): bit0 one MFMA product per block,
 // bit1 every k step re-reads the first step's A fragments (no L2 streaming).
+// acc *= 2^d (power of two: exact) — the move of the k-steps-0..7 partial sums from group A's
+// image scale to group B's at k step 8 (Scales2)
+template <int NQ>
+__device__ __forceinline__ void rescale_acc(floatx4 (&acc)[NQ][4], float f) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[q][cb] = acc[q][cb] * f;
+}
+
 template <bool PRIO, int NQ = 4, int EX = 0>
 __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
-                                            const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane) {
+                                            const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane,
+                                            float resc = 1.f) {
   constexpr int TS = (EX & 2) ? 0 : 1;
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -172,6 +183,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
       bh1[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * (t + 1));
       bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
     }
+    if (t == 8 && resc != 1.f) rescale_acc<NQ>(acc, resc);
     mfma3_step<PRIO, NQ, EX>(ah0, al0, bh0, bl0, acc);
     const int tn = (t + 2 < T) ? t + 2 : T - 1;
 #pragma unroll
@@ -196,7 +208,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
 // those of gemm16_tile.  The first step starts from an inline zero C operand.
 template <bool PRIO, int T, int NB>
 __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Float16* Hh, const _Float16* Hl,
-                                            floatx4 (&acc)[4][4], int lane) {
+                                            floatx4 (&acc)[4][4], int lane, float resc) {
   const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(base), 0, 4 * T * 2 * 1024, 0x00020000);
@@ -230,6 +242,7 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
         al[(j + NB - 1) % NB][q] = lda(q, t + NB - 1, 1);
       }
     }
+    if (!decltype(FIRST)::value && t == 8 && resc != 1.f) rescale_acc<4>(acc, resc);
     if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -264,15 +277,18 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
 }
 
 // acc = split product of the wave's 64 rows of packed matrix Wl (K = 32 T, T 16 or 14) and
-// the 64-point image: ring schedule with NB k steps in flight (NB 0: gemm16_tile)
+// the 64-point image: ring schedule with NB k steps in flight (NB 0: gemm16_tile).  `resc`
+// (a power of two) moves the partial sums from the image's group-A scale to its group-B
+// scale before k step 8 (Scales2); 1 for an image under one scale.
 template <bool PRIO, int NB>
 __device__ __forceinline__ void gemm16_sel(const _Float16* Wl, int w, int T, const _Float16* Hh,
-                                           const _Float16* Hl, floatx4 (&acc)[4][4], int lane) {
+                                           const _Float16* Hl, floatx4 (&acc)[4][4], int lane,
+                                           float resc = 1.f) {
   if constexpr (NB == 0) {
-    gemm16_tile<PRIO, 4>(wfrag(Wl, w, T), T, Hh, Hl, acc, lane);
+    gemm16_tile<PRIO, 4>(wfrag(Wl, w, T), T, Hh, Hl, acc, lane, resc);
   } else {
-    if (T != 14) gemm16_ring<PRIO, 16, NB>(Wl, w, Hh, Hl, acc, lane);
-    else gemm16_ring<PRIO, 14, NB>(Wl, w, Hh, Hl, acc, lane);
+    if (T != 14) gemm16_ring<PRIO, 16, NB>(Wl, w, Hh, Hl, acc, lane, resc);
+    else gemm16_ring<PRIO, 14, NB>(Wl, w, Hh, Hl, acc, lane, resc);
   }
 }
 
@@ -300,6 +316,33 @@ __device__ __forceinline__ int block_scale(float m, float* wmax, int w, int lane
 #pragma unroll
   for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, wmax[k]);
   return act_scale_exp(mm);
+}
+
+// Per-group scales of a forward activation image: rows 0..255 (waves 0-3, the next GEMM's
+// k steps 0..7) and rows 256..511 (waves 4-7, k steps 8..15) each from their own group's
+// max alone, capped at 2^30 (only an all-tiny group reaches the cap: its values then sit at
+// < 2^14 with 11-bit hi pieces and lo pieces down to 2^-27 absolute), so the k-step-8
+// rescale 2^(b - a) of the partial sums stays within fp32 for any finite activations below
+// 2^90.  Each group can split its rows without the other group's maximum — what a staggered
+// schedule needs; here, under the barrier, both are simply read.
+__device__ __forceinline__ int group_scale_exp(float m) { return min(act_scale_exp(m), 30); }
+
+struct Scales2 {
+  int a, b;
+  __device__ __forceinline__ int of(int w) const { return w < 4 ? a : b; }
+  __device__ __forceinline__ float resc() const { return ldexpf(1.f, b - a); }
+};
+__device__ __forceinline__ Scales2 block_scale2(float m, float* wmax, int w, int lane) {
+  m = wave_max(m, lane);
+  if (lane == 0) wmax[w] = m;
+  __syncthreads();
+  float ma = wmax[0], mb = wmax[4];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    ma = fmaxf(ma, wmax[k]);
+    mb = fmaxf(mb, wmax[4 + k]);
+  }
+  return Scales2{group_scale_exp(ma), group_scale_exp(mb)};
 }
 
 typedef float float2v __attribute__((ext_vector_type(2)));
@@ -424,9 +467,9 @@ struct NoStamp {
 
 // `stamp(phase)` marks phase ends for the DSR_EXP_STAMP diagnostic build (k_mlp_fwd16)
 template <class Stamp = NoStamp>
-__device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
-                                     Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk,
-                                     Stamp stamp = Stamp{}) {
+__device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
+                                         Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk,
+                                         Stamp stamp = Stamp{}) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
@@ -451,18 +494,12 @@ __device__ __forceinline__ int epi16(floatx4 (&acc)[4][4], int unscale, const fl
   }
   if (is_l3 && w == 6) xyz_rows(v, sm.xyz, lane, m);
   stamp(2);
-  m = wave_max(m, lane);
-  if (lane == 0) sm.wmax[w] = m;
-  __syncthreads();                       // all waves done reading H; maxima published
-  float mm = sm.wmax[0];
-#pragma unroll
-  for (int k = 1; k < NWAVE; ++k) mm = fmaxf(mm, sm.wmax[k]);
-  const int s = act_scale_exp(mm);
+  const Scales2 sc = block_scale2(m, sm.wmax, w, lane);   // all waves done reading H
   stamp(3);
-  write_split(v, s, sm.Hh, sm.Hl, w, lane);
+  write_split(v, sc.of(w), sm.Hh, sm.Hl, w, lane);
   stamp(4);
   mk = bits;
-  return s;
+  return sc;
 }
 
 // X: bit9 (512) exact re-decode of lite band samples — keep their ReLU masks + sdf
@@ -530,7 +567,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     __syncthreads();
     stamp(0);
     // ---- lin0 on VALU (fp32), then split
-    int sa;
+    Scales2 sa;
     MaskQueue mq;
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
@@ -555,8 +592,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           }
         }
       }
-      sa = block_scale(m, sm.wmax, w, lane);
-      write_split(v, sa, sm.Hh, sm.Hl, w, lane);
+      sa = block_scale2(m, sm.wmax, w, lane);
+      write_split(v, sa.of(w), sm.Hh, sm.Hl, w, lane);
       if constexpr (MSK) mask_push(mq, relu_bits(v));
     }
     __syncthreads();
@@ -565,10 +602,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     for (int l = 1; l <= 6; ++l) {
       const int lane = opaque(threadIdx.x & 63);
       stamp(7);
-      gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane);
+      gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
       uint64_t mk;
-      sa = epi16(acc, D.sw[l] + sa, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, stamp);
+      sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, stamp);
       if constexpr (MSK) mask_push(mq, mk);
       stamp(7);
       __syncthreads();
@@ -577,9 +614,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     {
       const int lane = opaque(threadIdx.x & 63);
       stamp(7);
-      gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane);
+      gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
-      const int un = D.sw[7] + sa;
+      const int un = D.sw[7] + sa.b;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
