@@ -56,17 +56,8 @@ static int split_ring() {
 using FwdKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                            const float*, float*, unsigned*, ErtArgs, MaskArgs);
 // split-fp16 forward with X's mask bit (512) and the ring depth in bits 10-11
-// DSR_SPLIT_STAGGER=1: the exact pass (kept masks) with staggered wave groups
-// (dsr_mlp16_st.hpp: k_mlp_fwd16_st, bitwise the barrier kernel on the 2-deep ring)
-static bool split_stagger() {
-  const char* e = getenv("DSR_SPLIT_STAGGER");
-  return e && atoi(e) == 1;
-}
 template <int MSK>
 static FwdKernel fwd16_kernel() {
-  if constexpr (MSK != 0) {
-    if (split_stagger() && split_ring() == 2) return k_mlp_fwd16_st<true, MSK | 1024>;
-  }
   switch (split_ring()) {
     case 2: return k_mlp_fwd16<true, MSK | 1024>;
     case 3: return k_mlp_fwd16<true, MSK | 2048>;

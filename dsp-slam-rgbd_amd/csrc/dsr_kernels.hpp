@@ -23,7 +23,6 @@
 #include "dsr_mlp.hpp"
 #include "dsr_mlp16.hpp"
 #include "dsr_mlp_lite.hpp"
-#include "dsr_mlp16_st.hpp"
 #include "../../include/dsr.h"
 
 // wave-wide 64-bit max (ockl DPP reduction; declared by HIP only under
