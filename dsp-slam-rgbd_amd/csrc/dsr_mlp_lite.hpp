@@ -459,13 +459,16 @@ __device__ __forceinline__ void st_signal(int* c) {
   asm volatile("" ::: "memory");
 }
 
+#ifndef DSR_LITE_WAIT_LOG2
+#define DSR_LITE_WAIT_LOG2 16
+#endif
 __device__ __forceinline__ void st_wait(int* c, int target, int* broken) {
   int n = 0;
   while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
          target) {
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
       break;
-    if (++n > (1 << 16)) {
+    if (++n > (1 << DSR_LITE_WAIT_LOG2)) {
       __hip_atomic_store(broken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       break;
     }
