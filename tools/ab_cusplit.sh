@@ -1,3 +1,5 @@
+# A/B of the DSR_CU_SPLIT experiment (object groups on even/odd CU halves via CU-masked streams),
+# measured and removed; the switch exists only in that experiment build, not in the product.
 set -u
 DSR_CU_SPLIT=0 timeout -k 10 120 python tools/batch_sig.py gpurun_out/cs_sig0.npz > gpurun_out/cs_sig.log 2>&1 || exit 1
 DSR_CU_SPLIT=1 timeout -k 10 120 python tools/batch_sig.py gpurun_out/cs_sig1.npz >> gpurun_out/cs_sig.log 2>&1 || exit 1
