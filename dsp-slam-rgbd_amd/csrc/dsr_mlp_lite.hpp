@@ -260,6 +260,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
   __shared__ LiteShared sm;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
+  if ((int)blockIdx.x >= nt) return;     // no tile for this block: skip the prologue (small passes)
   constexpr bool XL = (LV & 64) != 0;     // ring carried across layers, biases in LDS
   half8 ring[2][4];
   if constexpr (XL) {
@@ -501,6 +502,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = w >> 2;
   const int nt = *n_tiles;
+  if ((int)blockIdx.x >= nt) return;     // no tile for this block: skip the prologue (small passes)
   const int lag = E.lag;
   constexpr bool E2 = (LV & 256) != 0;
   constexpr int WS = E2 ? 1 : 2;
