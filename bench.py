@@ -19,8 +19,13 @@ also reports: the exact-decode leg (``value_exact``: DSR_LITE=0, every ray sampl
 decoded in 3xFP16), the three MFMA kernels' rooflines, the CPU baseline, and the
 Redwood keyframe leg (BASELINE config 5, ``keyframe``).
 
+Every N also runs a ``config4`` leg: BASELINE config 4 (64 objects x 4096 points, the same
+LPT sharding, 8 per GPU at N=8), so one N=1,2,4,8 sweep gives both strong-scaling curves.
+
 Usage: python bench.py [--gpus N --steps K --warmup W --objects B --pts P --weak]
-       (N>1 through torch.distributed.run, one process per GPU)
+       N>1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ranks are
+       the launcher's; without it bench.py starts ``torch.distributed.run --nproc-per-node N``
+       itself as a child process (before any GPU call) and exits with its status.
 """
 from __future__ import annotations
 
@@ -28,6 +33,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,6 +49,7 @@ import synthetic as S  # noqa: E402
 FWD_MAC = 1_769_984     # algorithmic forward MACs / point (code broadcast folded), SURVEY §8
 BWD_MAC = 1_835_520     # input-gradient backward MACs / point
 FP16_MFMA_PEAK_TF = 2500.0          # dense fp16/bf16 MFMA, spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TF = 157.3           # dense fp32 MFMA, spec
 FP16_MFMA_LOOP_TF = 1247.0          # the guide's bare 32x32x16 bf16 MFMA loop on random data (DVFS item 1)
 SPLIT_PRODUCTS = 3                  # 3xFP16: hi*hi + hi*lo + lo*hi per fp32 product
 DTYPE = ("fp16-mfma: 3xFP16 split (hi/lo fp16, fp32 accumulate) for every value that reaches "
@@ -139,7 +147,7 @@ def stats_sum(acc, st):
             acc[k] = max(acc.get(k, 0.0), v)
         elif k in ("lite_min_margin",):
             acc[k] = min(acc.get(k, 1e30), v)
-        elif k in ("lite", "keep_masks", "surface_in_exact"):
+        elif k in ("lite", "keep_masks", "surface_in_exact", "test_hooks"):
             acc[k] = v
         else:
             acc[k] = acc.get(k, 0) + v
@@ -246,6 +254,72 @@ def keyframe_leg(dec, n_keyframes=6, objects=4):
                     "detection in one async batch (includes H2D upload and result download)"}
 
 
+def spawn_ranks(n):
+    """``--gpus n`` without a launcher: run this script under torch.distributed.run with n
+    local ranks (RCCL rendezvous on 127.0.0.1) as a CHILD process — this process never
+    touches the GPU — and return its exit status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def fp32_algorithmic(a, steps, elapsed):
+    """SURVEY.md §8(d)'s algorithmic count: per object and iteration 2*1,769,984*(N + N_valid)
+    + 2*1,835,520*(N + K) FLOP (fp32 decoder, every in-ball sample decoded, Jacobian points
+    re-forwarded), summed over the timed steps, against the fp32 MFMA peak.  It exceeds that
+    peak because the build decodes fewer samples (exact early ray termination), classifies most
+    of them with one fp16 product and runs the rest as 3xFP16 — the fractions below."""
+    n, nv, k = a.get("jac_surface_points", 0), a.get("inball_points", 0), a.get("jac_render_points", 0)
+    flop = 2.0 * FWD_MAC * (n + nv) + 2.0 * BWD_MAC * (n + k)
+    tf = flop / elapsed / 1e12 if elapsed > 0 else 0.0
+    dec = a.get("fwd_points", 0)
+    return {"flop_per_step": flop / max(1, steps), "achieved_tflops": round(tf, 1),
+            "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TF, "frac_of_fp32_peak": round(tf / FP32_MFMA_PEAK_TF, 3),
+            "decoded_fraction_of_inball": round(dec / max(1, nv), 4),
+            "one_product_fraction_of_decoded": round(1.0 - a.get("refine_points", 0) / max(1, dec), 4)
+            if a.get("lite") else 0.0,
+            "note": "SURVEY §8(d) count over the timed steps / their time; > 1 of the fp32 peak because "
+                    "early ray termination skips samples and the lite pass classifies most decoded samples "
+                    "with one fp16 product (DESIGN.md §3.3-3.4)"}
+
+
+def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_pts=4096):
+    """BASELINE config 4: ONE job of 64 synthetic KITTI objects x 4096 points, LPT-sharded over
+    the ranks (8 per GPU at N=8) with the record gather; same timing rules as the main line."""
+    from reconstruct.parallel import ResidentShard
+
+    objs = []
+    for i in range(n_obj):
+        o = S.kitti_object(i, base_seed=3000, n_pts=n_pts)
+        objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
+    shard = ResidentShard(opt, objs, device=coll_dev)
+    try:
+        shard.run()                                   # warm-up
+        barrier()
+        t0 = time.perf_counter()
+        good = 0
+        for _ in range(steps):
+            res = shard.run()
+            if res is not None:
+                good += sum(int(r["is_good"]) for r in res)
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64, device=coll_dev or "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return {"value": n_obj * steps / el, "unit": "object-reconstructions/sec", "steps": steps,
+                "ms_per_step": el / steps * 1e3, "objects": n_obj, "pts": n_pts, "rays": n_pts + 200,
+                "shard_objects": [len(s) for s in shard.shards], "good_fraction": good / float(n_obj * steps),
+                "note": "BASELINE configs[3]: 64 x 4096-point objects, one job LPT-sharded over the ranks"}
+    finally:
+        shard.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,9 +330,15 @@ def main():
     ap.add_argument("--weak", action="store_true", help="every rank its own --objects objects")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the exact-decode and keyframe legs")
+    ap.add_argument("--no-config4", action="store_true", help="skip the 64 x 4096-point config-4 leg")
+    ap.add_argument("--dump-records", default="", help="rank 0 writes the last step's gathered records (.npy)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -307,9 +387,11 @@ def main():
     barrier()
     acc = {}
     n_good = 0
+    gather_s = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = shard.run()
+        gather_s += shard.last_gather_s
         if shard.handle is not None:
             st = L.Stats()
             ctx.check(lib.dsr_batch_stats(shard.handle, C.byref(st)), "stats")
@@ -318,10 +400,21 @@ def main():
             n_good += sum(int(r["is_good"]) for r in res)
     barrier()
     elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
+    ranks = {"world_size": world, "shard_objects": [len(s) for s in shard.shards],
+             "gather_ms_per_step": round(gather_s / args.steps * 1e3, 4)}
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev or "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        all_t = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(all_t, t)
+        per_rank = [float(x.item()) for x in all_t]
+        elapsed = max(per_rank)
+        ranks.update(backend=dist.get_backend(), world_size_observed=dist.get_world_size(),
+                     rank_seconds=[round(x, 4) for x in per_rank])
+    if args.dump_records and rank == 0 and res is not None:
+        np.save(args.dump_records, np.array([[r["loss"], float(r["is_good"]), r["iters_done"]]
+                                             + (list(np.asarray(r["t_cam_obj"]).reshape(-1)) + list(r["code"])
+                                                if r["is_good"] else [np.nan] * 80) for r in res], np.float32))
     value = n_job * args.steps / elapsed
     roof = kernel_rooflines(acc) if acc else {}
     loop = measured_mfma_loop(local) if rank == 0 and acc and not args.no_extra else None
@@ -336,6 +429,8 @@ def main():
         out = {
             "metric": f"object-reconstructions/sec ({args.pts} pts, 10 GN iters)",
             "value": value,
+            "value_basis": "inputs resident in HBM before the timed region (dsr_batch_create); "
+                           "host_inclusive_value adds the PCIe upload (SURVEY §8(d) end-to-end)",
             "unit": "object-reconstructions/sec",
             "n_gpus": world,
             "steps": args.steps,
@@ -374,6 +469,10 @@ def main():
                 "max_observed_lite_error": acc["lite_max_err"], "min_margin": acc["lite_min_margin"]},
             "jac_points": {"surface": acc.get("jac_surface_points"), "render": acc.get("jac_render_points"),
                            "render_backward_only": bool(acc.get("keep_masks"))},
+            "fp32_algorithmic": fp32_algorithmic(acc, args.steps, elapsed) if acc else None,
+            "lite_broken_blocks": acc.get("lite_broken_blocks"),
+            "test_hooks": acc.get("test_hooks"),
+            "ranks": ranks,
             "good_fraction": n_good / float(n_job * args.steps),
             # inputs handed over in host memory: the upload added to one step
             "host_inclusive_value": n_job / (elapsed / args.steps + create_s),
@@ -385,6 +484,10 @@ def main():
             out["roofline"]["traffic"] = tr[0]
             out["roofline"]["traffic_source"] = tr[1]
     shard.close()
+    if not args.no_config4 and not args.weak:
+        c4 = config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=min(args.steps, 3))
+        if rank == 0:
+            out["config4"] = c4
     if world == 1 and not args.no_extra:
         # exact-decode leg: DSR_LITE=0 (every in-ball sample decoded in 3xFP16), same job
         os.environ["DSR_LITE"] = "0"

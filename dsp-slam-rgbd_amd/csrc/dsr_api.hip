@@ -10,6 +10,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -39,6 +40,9 @@ struct dsr_ctx {
   std::multimap<size_t, void*> pool;      // free device blocks by size
   size_t pool_bytes = 0;
   std::vector<hipEvent_t> ev_timing, ev_plain;
+  // guards pool / ev_*: a context is used from one thread at a time (include/dsr.h), but
+  // batches of async handles may be destroyed from another Python thread (finalizers)
+  std::mutex mu;
 };
 static constexpr size_t POOL_CAP = (size_t)16 << 30;
 
@@ -132,12 +136,19 @@ static bool refine_all() {
   const char* e = getenv("DSR_REFINE_ALL");
   return e && atoi(e) != 0;
 }
+// Test hooks (DSR_LITE_PERTURB, DSR_LITE_BREAK) change results or cost on purpose; the library
+// honours them only when DSR_TEST_HOOKS=1 was set as the batch was created, and reports that
+// in dsr_stats.test_hooks, so a stray variable cannot silently change a production run.
+static bool test_hooks() {
+  const char* e = getenv("DSR_TEST_HOOKS");
+  return e && atoi(e) != 0;
+}
 // DSR_LITE_LAG (staggered lite kernel): the k step group A reaches before group B starts a GEMM.
 // DSR_LITE_BREAK=1 (test hook): every block starts in the "broken" state of a timed-out
 // event wait, so every sample goes to the exact pass (lag -1)
-static int lite_lag() {
+static int lite_lag(bool hooks) {
   const char* b = getenv("DSR_LITE_BREAK");
-  if (b && atoi(b) != 0) return -1;
+  if (hooks && b && atoi(b) != 0) return -1;
   const char* e = getenv("DSR_LITE_LAG");
   const int v = e ? atoi(e) : 4;
   return v < 0 ? 0 : (v > 7 ? 7 : v);
@@ -214,6 +225,11 @@ struct dsr_batch {
   bool lite = true;             // lite classification pass + exact re-decode of the band
   int loop_iters = 0;           // iters + 1 spare iteration for audit redos (lite + audit)
   bool spare_run = false;       // the spare iteration was enqueued for the last run
+  // lite-pass settings fixed at creation (the iteration count, event sizing and the spare
+  // iteration depend on them, so a run never re-reads the environment)
+  ErtArgs lite_cfg{};           // audit, shell, audit_log2, perturb, lag
+  bool hooks = false;           // DSR_TEST_HOOKS=1 at creation
+  int* diag = nullptr;          // [STD_INTS] broken-block count + first expired wait (dsr_dev.hpp)
   std::vector<int> passes;      // render-pass rank boundaries, last = M
   std::vector<hipEvent_t> ev;   // begin, end, then per (iteration, group): fwd0/fwd1 per pass, jac0, jac1
   bool ran = false;
@@ -556,6 +572,7 @@ static size_t ev_per_iter(const dsr_batch* b) { return 2 * (b->passes.size() - 1
 // plus 1 MB), else hipMalloc.
 static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
   dsr_ctx* ctx = b->ctx;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
   auto it = ctx->pool.lower_bound(bytes);
   if (it != ctx->pool.end() && it->first <= 2 * bytes + ((size_t)1 << 20)) {
@@ -565,11 +582,22 @@ static int batch_alloc(dsr_batch* b, void** p, size_t bytes) {
     ctx->pool.erase(it);
     return 0;
   }
-  if (hipMalloc(p, bytes) != hipSuccess) return fail(ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    // pooled blocks that did not fit may be what fills the device: return them and retry once
+    (void)hipGetLastError();
+    for (auto& kv : ctx->pool) hipFree(kv.second);
+    ctx->pool.clear();
+    ctx->pool_bytes = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(ctx, "hipMalloc failed (" + std::to_string(bytes) + " B)");
+    }
+  }
   b->allocs.emplace_back(*p, bytes);
   return 0;
 }
 static hipError_t pool_event(dsr_ctx* ctx, hipEvent_t* e, bool timing) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
   auto& v = timing ? ctx->ev_timing : ctx->ev_plain;
   if (!v.empty()) {
     *e = v.back();
@@ -582,18 +610,16 @@ static hipError_t pool_event(dsr_ctx* ctx, hipEvent_t* e, bool timing) {
 // Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
 // (1.0): out-of-band samples with |y| < th + shell*margin are audited; DSR_LITE_AUDIT_LOG2
 // (7): plus a hashed 2^-log2 share of all other decoded samples; DSR_LITE_PERTURB: test hook
-static void lite_audit_args(ErtArgs& E) {
+static ErtArgs lite_settings(bool hooks) {
   auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
+  ErtArgs E{};
   const char* a = getenv("DSR_LITE_AUDIT");
   E.audit = (a && atoi(a) == 0) ? 0 : 1;
   E.shell = envf("DSR_LITE_SHELL", 1.0f);
   E.audit_log2 = std::max(0, std::min(24, (int)envf("DSR_LITE_AUDIT_LOG2", 7.0f)));
-  E.perturb = envf("DSR_LITE_PERTURB", 0.0f);
-}
-static bool lite_audit_on() {
-  ErtArgs E{};
-  lite_audit_args(E);
-  return E.audit != 0;
+  E.perturb = hooks ? envf("DSR_LITE_PERTURB", 0.0f) : 0.0f;
+  E.lag = lite_lag(hooks);
+  return E;
 }
 
 static GNParams make_params(const dsr_optim_params* p) {
@@ -618,6 +644,7 @@ int dsr_batch_destroy(dsr_batch* b) {
   // the blocks go back to the pool: no kernel of this batch may still be using them
   for (size_t g = 0; g < std::max<size_t>(1, b->groups.size()); ++g) hipStreamSynchronize(ctx->gstream[g]);
   if (b->graph) hipGraphExecDestroy(b->graph);
+  std::lock_guard<std::mutex> lk(ctx->mu);
   for (auto& e : b->ev)
     if (e) ctx->ev_timing.push_back(e);
   for (hipEvent_t e : b->join_ev)
@@ -786,7 +813,10 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
   ALLOC(b->sred, sizeof(float) * 2 * SLOT_FLOATS * (size_t)n_obj);
-  b->loop_iters = b->iters + ((b->lite && lite_audit_on() && b->iters > 0) ? 1 : 0);
+  b->hooks = test_hooks();
+  b->lite_cfg = lite_settings(b->hooks);
+  b->loop_iters = b->iters + ((b->lite && b->lite_cfg.audit && b->iters > 0) ? 1 : 0);
+  ALLOC(b->diag, sizeof(int) * STD_INTS);
   ALLOC(b->counts, sizeof(int) * NCOUNT * (size_t)std::max(1, b->loop_iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
   if (trace) {
@@ -886,7 +916,13 @@ int dsr_batch_graph(dsr_batch* b) {
 
 static int batch_launch(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
-  if (!graph_enabled() || b->runs++ == 0) return batch_enqueue(b);
+  if (!graph_enabled() || b->runs++ == 0) {
+    const int rc = batch_enqueue(b);
+    if (rc) return rc;
+    b->ran = true;
+    b->timed = true;
+    return 0;
+  }
   if (!b->graph || b->graph_key != graph_key()) {
     const int rc = batch_capture(b);
     if (rc) return rc;
@@ -894,6 +930,7 @@ static int batch_launch(dsr_batch* b) {
   DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
   DSR_CHECK(ctx, hipGraphLaunch(b->graph, ctx->stream));
   DSR_CHECK(ctx, hipEventRecord(b->ev[1], ctx->stream));
+  b->spare_run = false;          // a replay runs the regular iterations only (batch_finish)
   b->ran = true;
   b->timed = false;
   return 0;
@@ -909,14 +946,18 @@ int dsr_batch_run(dsr_batch* b) {
   return 0;
 }
 
+static int batch_redo(dsr_batch* b);
+
 int dsr_batch_query(dsr_batch* b) {
   if (!b) return -2;
   if (!b->ran) return fail(b->ctx, "batch has not run");
   hipSetDevice(b->ctx->device);
   const hipError_t e = hipEventQuery(b->done_ev);
   if (e == hipSuccess) {
-    const int rc = batch_finish(b);        // a pending redo is enqueued (and waited) here
-    return rc ? rc : 1;
+    // a pending audit redo is enqueued here and the batch reported as still in flight: the
+    // caller's next query sees it finish (never blocks for a GN iteration)
+    const int rc = batch_redo(b);
+    return rc < 0 ? rc : (rc == 1 ? 0 : 1);
   }
   if (e == hipErrorNotReady) return 0;
   return fail(b->ctx, std::string("hipEventQuery: ") + hipGetErrorString(e));
@@ -930,17 +971,18 @@ static int batch_enqueue(dsr_batch* b, bool timing) {
   if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
   hipLaunchKernelGGL(k_init_state, dim3(n), dim3(64), 0, ctx->stream, n, b->t_in, b->is_oc, b->z_in, b->st,
                      b->zbuf, b->iters);
+  DSR_CHECK(ctx, hipMemsetAsync(b->diag, 0, sizeof(int) * STD_INTS, ctx->stream));
   b->spare_run = false;
   return batch_enqueue_iters(b, timing, 0, b->iters);
 }
 
 // The spare iteration (lite + audit): only objects whose iteration an audit discarded
-// (k_solve) are still running after the regular iterations.  It is enqueued on demand
-// when the host waits for the batch (batch_finish), so a run without violations launches
-// nothing extra; graphs capture the regular iterations only.
-static int batch_finish(dsr_batch* b) {
+// (k_solve) are still running after the regular iterations.  It is enqueued on demand once
+// the regular iterations have finished (batch_finish, dsr_batch_query), so a run without
+// violations launches nothing extra; graphs capture the regular iterations only.
+// Returns 1 if the spare iteration was enqueued now, 0 if there is nothing to redo.
+static int batch_redo(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
-  DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   if (b->loop_iters <= b->iters || b->spare_run) return 0;
   std::vector<ObjState> hs(b->n_obj);
   DSR_CHECK(ctx, hipMemcpy(hs.data(), b->st, sizeof(ObjState) * hs.size(), hipMemcpyDeviceToHost));
@@ -950,7 +992,15 @@ static int batch_finish(dsr_batch* b) {
   b->spare_run = true;
   const int rc = batch_enqueue_iters(b, b->timed, b->iters, b->loop_iters);
   if (rc) return rc;
+  DSR_CHECK(ctx, hipEventRecord(b->done_ev, ctx->stream));
+  return 1;
+}
+static int batch_finish(dsr_batch* b) {
+  dsr_ctx* ctx = b->ctx;
   DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  const int rc = batch_redo(b);
+  if (rc < 0) return rc;
+  if (rc == 1) DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   return 0;
 }
 
@@ -983,8 +1033,13 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       float* b4 = b->bias4f + (size_t)o0 * HID;
       hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
       hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
-      ErtArgs ert{b->dead, b->M, -P.cut_off, b->lite ? st : nullptr, b->refine, lite_lag()};
-      lite_audit_args(ert);
+      ErtArgs ert = b->lite_cfg;
+      ert.dead = b->dead;
+      ert.M = b->M;
+      ert.nth = -P.cut_off;
+      ert.st = b->lite ? st : nullptr;
+      ert.refine = b->refine;
+      ert.diag = b->diag;
       DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
                                        (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
@@ -1050,8 +1105,6 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
   hipLaunchKernelGGL(k_finalize, dim3(cb), dim3(64), 0, s0, n, b->st, b->zbuf, b->out);
   DSR_CHECK(ctx, hipGetLastError());
   if (timing) DSR_CHECK(ctx, hipEventRecord(b->ev[1], s0));
-  b->ran = true;
-  b->timed = timing;
   return 0;
 }
 
@@ -1112,6 +1165,12 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->jac_launches = b->timed ? used_iters * G : 0;
   st->refine_launches = (b->timed && b->lite) ? used_iters * G : 0;
   st->lite = b->lite ? 1 : 0;
+  st->test_hooks = b->hooks ? 1 : 0;
+  {
+    int nb = 0;
+    DSR_CHECK(b->ctx, hipMemcpy(&nb, b->diag + STD_BROKEN, sizeof(int), hipMemcpyDeviceToHost));
+    st->lite_broken_blocks = nb;
+  }
   st->keep_masks = (b->lite && b->ma.msk && fwd_variant() == 12) ? 1 : 0;
   st->surface_in_exact = (st->keep_masks && b->ma.pts && jac_variant() == 12) ? 1 : 0;
   if (b->lite) {
@@ -1136,6 +1195,19 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
       st->jac_render_points += e[5];
       st->jac_surface_points += e[1] - e[5];
     }
+  return 0;
+}
+
+int dsr_batch_lite_diag(dsr_batch* b, int* rec, int n) {
+  if (!b || !rec || n < 0) return -2;
+  if (!b->ran) return fail(b->ctx, "batch has not run");
+  hipSetDevice(b->ctx->device);
+  {
+    const int rc = batch_finish(b);
+    if (rc) return rc;
+  }
+  const int k = std::min(n, (int)STD_INTS);
+  DSR_CHECK(b->ctx, hipMemcpy(rec, b->diag, sizeof(int) * k, hipMemcpyDeviceToHost));
   return 0;
 }
 

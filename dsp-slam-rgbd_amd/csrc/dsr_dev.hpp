@@ -111,7 +111,21 @@ struct ErtArgs {
   int audit;             // 0: no audit
   float shell;
   int audit_log2;
-  float perturb;         // test hook (DSR_LITE_PERTURB): lite values moved by +-perturb
+  float perturb;         // test hook (DSR_LITE_PERTURB, only with DSR_TEST_HOOKS=1): lite values moved by +-perturb
+  int* diag;             // staggered lite pass: [0] blocks whose event wait expired, [1..] the first
+                         // expired wait's record (StDiag, dsr_mlp_lite.hpp); nullptr: none kept
+};
+
+// Record of the first expired event wait of a batch run (k_mlp_fwd_lite_st, st_wait), in
+// ErtArgs.diag.  Read by dsr_batch_stats (dsr_stats.lite_broken_blocks) and the diagnostics
+// entry point dsr_batch_lite_diag.
+enum {
+  STD_BROKEN = 0,        // blocks that marked themselves broken (all launches of the run)
+  STD_CLAIM,             // 1 once the record below is written
+  STD_BLOCK, STD_WAVE, STD_COUNTER, STD_TARGET, STD_OBSERVED, STD_IT, STD_HWID, STD_XCC,
+  STD_POLLS,             // polls from the clock start (poll 1024) to expiry
+  STD_REAL,              // 100 MHz ticks (s_memrealtime) over those polls
+  STD_INTS
 };
 
 // bit 30 of a refine candidate's sample index (cand[].w): the sample is an audit, not a band sample
@@ -134,7 +148,8 @@ __device__ __forceinline__ unsigned char lite_flag(const ErtArgs& E, float y, in
   return au ? (full ? 3 : 2) : 0;
 }
 
-// test hook: a deterministic +-perturb on every lite value (DSR_LITE_PERTURB)
+// test hook: a deterministic +-perturb on every lite value (DSR_LITE_PERTURB; the library
+// honours it only under DSR_TEST_HOOKS=1, which dsr_stats.test_hooks reports)
 __device__ __forceinline__ float lite_perturb(const ErtArgs& E, float y, int idx) {
   if (E.perturb == 0.f) return y;
   return y + ((((unsigned)idx * 2654435761u) >> 31) ? E.perturb : -E.perturb);

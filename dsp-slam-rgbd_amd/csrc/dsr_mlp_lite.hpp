@@ -452,6 +452,9 @@ struct LiteStShared {
   float w8[HID];
   int ovf[2];                  // per tile parity: (tile iteration + 1) if a value reached 2^15
   int cH[2], cRlo, cRhi, cP, cT[2], cE, broken, pad[7];
+  unsigned twait[NWAVE];       // 100 MHz time at which a wave's current wait passed 1024 polls
+  int rec[6];                  // the block's first expired wait: counter, target, observed, tile
+                               // iteration, wave (-1: none), 100 MHz ticks
 };
 
 __device__ __forceinline__ void st_signal(int* c) {
@@ -463,14 +466,54 @@ __device__ __forceinline__ void st_signal(int* c) {
 #ifndef DSR_LITE_WAIT_LOG2
 #define DSR_LITE_WAIT_LOG2 16
 #endif
-__device__ __forceinline__ void st_wait(int* c, int target, int* broken) {
+// The wave whose wait expires first breaks its block and notes in LDS which counter it waited
+// on, the target and the value it saw, the tile iteration, itself, the real time its last
+// 2^16 - 1024 polls took (a poll is one s_sleep 1 + one LDS load, ~0.1 us: far more time than
+// that means the wave was not running).  (A snapshot of all counters here doubled the kernel's
+// register spills, so the record holds the waited-on counter only.)
+// At its exit the same wave counts the block in diag[STD_BROKEN] and, if it is the run's
+// first, copies the note to diag (st_report) — the global writes stay out of the GEMM loop.
+__device__ __forceinline__ void st_expire(int* c, int target, int observed, LiteStShared& sm, int it, int w) {
+  int prev = 0;
+  if (__lane_id() == 0) prev = __hip_atomic_exchange(&sm.broken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  prev = __builtin_amdgcn_readfirstlane(prev);
+  if (prev != 0 || __lane_id() != 0) return;
+  sm.rec[0] = (int)(c - &sm.ovf[0]);
+  sm.rec[1] = target;
+  sm.rec[2] = observed;
+  sm.rec[3] = it;
+  sm.rec[5] = (int)((unsigned)__builtin_amdgcn_s_memrealtime() - sm.twait[w]);
+  sm.rec[4] = w;
+}
+
+__device__ __forceinline__ void st_report(const LiteStShared& sm, int* diag, int w) {
+  if (diag == nullptr || sm.rec[4] != w || __lane_id() != 0) return;
+  atomicAdd(diag + STD_BROKEN, 1);
+  if (atomicCAS(diag + STD_CLAIM, 0, 1) != 0) return;
+  diag[STD_BLOCK] = (int)blockIdx.x;
+  diag[STD_WAVE] = w;
+  diag[STD_COUNTER] = sm.rec[0];
+  diag[STD_TARGET] = sm.rec[1];
+  diag[STD_OBSERVED] = sm.rec[2];
+  diag[STD_IT] = sm.rec[3];
+  diag[STD_HWID] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID: wave / SIMD / CU / SE
+  diag[STD_XCC] = (int)__builtin_amdgcn_s_getreg((31 << 11) | 20);     // XCC_ID
+  diag[STD_POLLS] = (1 << DSR_LITE_WAIT_LOG2) - 1024;
+  diag[STD_REAL] = sm.rec[5];
+  __threadfence();
+}
+
+__device__ __forceinline__ void st_wait(int* c, int target, LiteStShared& sm, int it, int w) {
   int n = 0;
-  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+  int v;
+  while ((v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) <
          target) {
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&sm.broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
       break;
-    if (++n > (1 << DSR_LITE_WAIT_LOG2)) {
-      __hip_atomic_store(broken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    ++n;
+    if (n == 1024) sm.twait[w] = (unsigned)__builtin_amdgcn_s_memrealtime();   // a long wait: clock it
+    if (n > (1 << DSR_LITE_WAIT_LOG2)) {
+      st_expire(c, target, v, sm, it, w);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -515,10 +558,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       if (l < 6) sm.bias[l < 3 ? l + 1 : l + 2][n] = D.bias[l < 3 ? l + 1 : l + 2][n];
       else sm.w8[n] = D.W8[n];
     }
-    if (tid < 18) {   // counters and flags; DSR_LITE_BREAK test hook: start broken
+    if (tid < 18) {   // counters and flags; DSR_LITE_BREAK test hook: start broken (and count it)
       int* f = &sm.ovf[0] + tid;
       *f = (f == &sm.broken && E.lag < 0) ? 1 : 0;
+      if (f == &sm.broken && E.lag < 0 && E.diag) atomicAdd(E.diag + STD_BROKEN, 1);
     }
+    if (tid == 18) sm.rec[4] = -1;
     const int lane = tid & 63;
     const _Float16* A1 = WA[1] + (size_t)(4 * w) * (D.Kf[1] / 32) * WS * 64 * 8;
     const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
@@ -534,6 +579,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
 #endif
   int it = 0;
+  auto wait = [&](int* c, int target) { st_wait(c, target, sm, it, w); };
   for (int ti = blockIdx.x; ti < nt; ti += gridDim.x, ++it) {
     const int p = it & 1;
     const Tile tl = tiles[ti];
@@ -543,7 +589,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
     // ---- tile inputs, per group
     {
       const int lane = opaque(threadIdx.x & 63);
-      if (grp == 1) st_wait(&sm.cE, 4 * it, &sm.broken);
+      if (grp == 1) wait(&sm.cE, 4 * it);
       const int gt = opaque(threadIdx.x) & 255;
       if (gt < LTILE) {
         const float4 v = (gt < tl.count) ? cand[d.cand_off + tl.start + gt] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -554,7 +600,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         *reinterpret_cast<float4*>(&sm.bias[which == 0 ? 0 : 4][n]) = *reinterpret_cast<const float4*>(src);
       }
       st_signal(&sm.cT[grp]);
-      st_wait(&sm.cT[grp], 4 * (it + 1), &sm.broken);
+      wait(&sm.cT[grp], 4 * (it + 1));
     }
     LSTAMP(0)
     floatx4 acc[4][8];
@@ -587,7 +633,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
       LSTAMP(1)
-      st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * 7 * it, &sm.broken);   // readers of lin7's input
+      wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * 7 * it);   // readers of lin7's input
       LSTAMP(2)
       lite_write<(LV & 1024) != 0>(acc, 0, sm.H, w, lane);
       st_signal(&sm.cH[grp]);
@@ -597,10 +643,10 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
     auto gemm = [&](int l) {
       const int ng = 7 * it + l;         // GEMMs so far, this one included
       const int hs = 4 * (8 * it + l);   // cH count once the input image is complete
-      st_wait(&sm.cH[0], hs, &sm.broken);
+      wait(&sm.cH[0], hs);
       if (grp == 1) {
-        st_wait(&sm.cH[1], hs, &sm.broken);
-        if (lag > 0) st_wait(&sm.cP, 4 * ng, &sm.broken);
+        wait(&sm.cH[1], hs);
+        if (lag > 0) wait(&sm.cP, 4 * ng);
       }
       LSTAMP(4)
       auto hook = [&](int t) {
@@ -608,12 +654,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         if (t == 7 && grp == 0) {
           __builtin_amdgcn_sched_barrier(0);
           const unsigned long long h0 = __builtin_amdgcn_s_memtime();
-          st_wait(&sm.cH[1], hs, &sm.broken);
+          wait(&sm.cH[1], hs);
           stamp[8] += __builtin_amdgcn_s_memtime() - h0;
           __builtin_amdgcn_sched_barrier(0);
         }
 #else
-        if (t == 7 && grp == 0) st_wait(&sm.cH[1], hs, &sm.broken);
+        if (t == 7 && grp == 0) wait(&sm.cH[1], hs);
 #endif
         if (t == 8) st_signal(&sm.cRlo);
         if (t == lag && grp == 0) st_signal(&sm.cP);
@@ -665,7 +711,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         }
         if (!(__int_as_float(mi) < 32768.f)) sm.ovf[p] = it + 1;
         LSTAMP(6)
-        st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
+        wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l));
         LSTAMP(2)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -709,7 +755,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
         }
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
-      st_wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l), &sm.broken);
+      wait(grp == 0 ? &sm.cRlo : &sm.cRhi, 8 * (7 * it + l));
       lite_write<(LV & 1024) != 0>(acc, 0, sm.H, w, lane);
       st_signal(&sm.cH[grp]);
     }
@@ -747,8 +793,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
     if (grp == 1) {
       const int lane = opaque(threadIdx.x & 63);
       if (w < 6) {
-        st_wait(&sm.cH[0], 4 * (8 * it + 8), &sm.broken);
-        st_wait(&sm.cH[1], 4 * (8 * it + 8), &sm.broken);
+        wait(&sm.cH[0], 4 * (8 * it + 8));
+        wait(&sm.cH[1], 4 * (8 * it + 8));
         const int tid = opaque(threadIdx.x) - 256;
         if (tid < tl.count) {
           float s = sm.red[tid];
@@ -772,6 +818,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
       st_signal(&sm.cE);
     }
   }
+  st_report(sm, E.diag, w);
 #ifdef DSR_EXP_STAMP
   LSTAMP(7)
   if (blockIdx.x < 4 && (threadIdx.x == 0 || threadIdx.x == 256))

@@ -9,7 +9,9 @@ Data ingest (KITTI / Redwood sequences, mmdet detectors — reference
 (SURVEY.md §2 rows 9-12).  When ``DSR_REFERENCE_RECONSTRUCT`` points at the
 reference's ``reconstruct/`` directory, ``get_sequence`` / ``get_detectors`` (same
 dispatch as the reference's ``reconstruct/__init__.py:1-22``) load exactly those four
-named ingest modules from there.  Nothing else is ever resolved outside this package:
+named ingest modules from there.  The host helpers they import from this package exist
+here (``reconstruct.loss_utils.get_rays / get_time``, ``reconstruct.utils.read_calib_file /
+load_velo_scan / ForceKeyErrorDict``).  Nothing else is ever resolved outside this package:
 a missing ``reconstruct.<name>`` (e.g. ``loss``) is an ImportError, never the
 reference's torch code.
 """

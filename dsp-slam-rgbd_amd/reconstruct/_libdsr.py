@@ -67,7 +67,7 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 5          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 6          # include/dsr.h DSR_ABI_VERSION
 
 
 class Stats(C.Structure):
@@ -79,7 +79,15 @@ class Stats(C.Structure):
                 ("lite_min_margin", C.c_double), ("jac_surface_points", C.c_int64),
                 ("jac_render_points", C.c_int64), ("keep_masks", C.c_int),
                 ("lite_audit_violations", C.c_int), ("lite_redo_objects", C.c_int),
-                ("surface_in_exact", C.c_int), ("audit_points", C.c_int64)]
+                ("surface_in_exact", C.c_int), ("audit_points", C.c_int64),
+                ("lite_broken_blocks", C.c_int), ("test_hooks", C.c_int)]
+
+#: dsr_batch_lite_diag record layout (csrc/dsr_dev.hpp: STD_*)
+LITE_DIAG_FIELDS = ("broken_blocks", "recorded", "block", "wave", "counter", "target", "observed", "tile_iter",
+                    "hw_id", "xcc_id", "polls", "real_ticks")
+#: the counter index (``counter``) names the LiteStShared event counter that was waited on
+LITE_DIAG_COUNTERS = ("ovf0", "ovf1", "cH0", "cH1", "cRlo", "cRhi", "cP", "cT0", "cT1", "cE", "broken")
+LITE_DIAG_INTS = len(LITE_DIAG_FIELDS)
 
 
 #: every function declared in include/dsr.h, with its ctypes signature
@@ -103,6 +111,7 @@ SIGNATURES = {
     "dsr_batch_query": (C.c_int, [C.c_void_p]),
     "dsr_batch_download": (C.c_int, [C.c_void_p, C.POINTER(ObjectOut)]),
     "dsr_batch_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "dsr_batch_lite_diag": (C.c_int, [C.c_void_p, IP, C.c_int]),
     "dsr_batch_destroy": (C.c_int, [C.c_void_p]),
     "dsr_sdf_eval": (C.c_int, [C.c_void_p, C.c_void_p, FP, FP, C.c_int, FP, FP]),
     "dsr_pose_only": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), FP, C.c_float,
@@ -187,6 +196,20 @@ class Context:
         if rc != 0:
             msg = self.lib.dsr_last_error(self.handle)
             raise DsrError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def lite_diag(lib, handle):
+    """The last run's staggered-lite-pass record (dsr_batch_lite_diag) as a dict."""
+    rec = (C.c_int * LITE_DIAG_INTS)()
+    rc = lib.dsr_batch_lite_diag(handle, rec, LITE_DIAG_INTS)
+    if rc != 0:
+        raise DsrError(f"dsr_batch_lite_diag failed ({rc})")
+    v = list(rec)
+    d = dict(zip(LITE_DIAG_FIELDS, v))
+    if d["recorded"] and 0 <= d["counter"] < len(LITE_DIAG_COUNTERS):
+        d["counter"] = LITE_DIAG_COUNTERS[d["counter"]]
+    d["real_us"] = (d.pop("real_ticks") & 0xffffffff) / 100.0      # 100 MHz counter
+    return d
 
 
 def optim_params(cfg) -> OptimParams:

@@ -106,6 +106,7 @@ class ResidentShard:
         self.width = max(len(s) for s in self.shards)
         self._keep = []
         self.handle = None
+        self.last_gather_s = 0.0
         self.outs = (L.ObjectOut * max(1, len(self.mine)))()
         if self.mine:
             ins = (L.ObjectIn * len(self.mine))()
@@ -138,12 +139,18 @@ class ResidentShard:
         return rec
 
     def run(self):
-        """One step: launch, wait, gather. Results in input order on rank 0, None elsewhere."""
+        """One step: launch, wait, gather. Results in input order on rank 0, None elsewhere.
+        ``last_gather_s`` holds the host time of this step's gather (the RCCL collective)."""
+        import time
+
         self.launch()
         rec = self.records()
         if not self.dist:
+            self.last_gather_s = 0.0
             return unpack_all(rec, self.n)
+        t0 = time.perf_counter()
         allrec = gather_records(rec, self.width, self.group, self.device)
+        self.last_gather_s = time.perf_counter() - t0
         return None if allrec is None else unpack_all(allrec, self.n)
 
     def close(self):

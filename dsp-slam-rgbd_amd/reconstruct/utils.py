@@ -1,4 +1,4 @@
-"""Config / decoder factory half of ``reconstruct/utils.py`` (utils.py:82-116).
+"""Config / decoder factory half of ``reconstruct/utils.py`` (utils.py:58-116).
 
 Same names and behaviour the C++ side relies on (src/System.cc:95-98):
 ``get_configs(path)`` returns an attribute dict that raises ``KeyError`` on a
@@ -41,6 +41,28 @@ class ForceKeyErrorDict(dict):
 
     def __missing__(self, key):
         raise KeyError(key)
+
+
+def read_calib_file(filepath):
+    """utils.py:58-73: a KITTI calibration file as {key: float64 array}; parsing stops at the
+    first empty line and keys whose values are not all numbers (dates) are skipped.  Used by
+    the reference's kitti_sequence.py (data ingest, kept by the C++ caller)."""
+    data = {}
+    with open(filepath, "r") as f:
+        for line in f.readlines():
+            if line == "\n":
+                break
+            key, value = line.split(":", 1)
+            try:
+                data[key] = np.array([float(x) for x in value.split()])
+            except ValueError:
+                pass
+    return data
+
+
+def load_velo_scan(file):
+    """utils.py:76-79: a velodyne .bin scan as an (N, 4) float32 array (x, y, z, reflectance)."""
+    return np.fromfile(file, dtype=np.float32).reshape((-1, 4))
 
 
 def get_configs(cfg_file):

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 5
+#define DSR_ABI_VERSION 6
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -142,6 +142,11 @@ typedef struct {
   int surface_in_exact;           /* 1: the exact pass ran the surface points' forward too and
                                      the Jacobian kernel only backward chains (kept masks) */
   int64_t audit_points;           /* out-of-band samples re-decoded exactly as an audit */
+  int lite_broken_blocks;         /* staggered lite-pass workgroups whose bounded event wait
+                                     expired in the last run (their samples all went to the
+                                     exact pass: results stay exact, the cost rises); 0 expected */
+  int test_hooks;                 /* 1: the batch was created with DSR_TEST_HOOKS=1, so the test
+                                     hooks DSR_LITE_PERTURB / DSR_LITE_BREAK were honoured */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */
@@ -179,6 +184,12 @@ int dsr_batch_query(dsr_batch* b);                /* 1: the last run has finishe
                                                       flight (host work can overlap it), <0 error */
 int dsr_batch_download(dsr_batch* b, dsr_object_out* out);
 int dsr_batch_stats(dsr_batch* b, dsr_stats* st);
+/* Diagnostics of the staggered lite pass (no reference counterpart): copies up to n ints of
+ * the last run's record — [0] broken workgroups, [1] 1 if the first expired event wait was
+ * recorded, then its workgroup, wave, counter, target, observed value, tile iteration,
+ * HW_ID, XCC_ID, and how many polls took how many 100 MHz ticks before it expired
+ * (csrc/dsr_dev.hpp: STD_*; 16 ints). */
+int dsr_batch_lite_diag(dsr_batch* b, int* rec, int n);
 int dsr_batch_destroy(dsr_batch* b);
 
 /* ---- decoder queries: replaces decode_sdf / get_batch_sdf_jacobian

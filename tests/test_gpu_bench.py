@@ -1,0 +1,50 @@
+"""bench.py's multi-rank path on one GPU (the driver's N>1 runs use RCCL over xGMI, one GPU
+per rank; here two gloo ranks share device 0, which RCCL refuses).
+
+``python bench.py --gpus 2`` with no launcher starts torch.distributed.run itself; each rank
+uploads its LPT shard (reconstruct/parallel.py: ResidentShard), and one all-gather returns
+every object's record to rank 0.  The gathered records must be bitwise those of a
+one-process run of the same job — objects never interact, and a batch's
+results do not depend on how the objects are split into batches (test_batch_equals_single).
+This replaces the reference's sequential per-detection loop
+(/root/reference/src/LocalMapping_util.cc:165-206) with object-sharded ranks.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench(n, dump, extra=()):
+    env = dict(os.environ, DSR_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0", "--objects", "8",
+           "--no-extra", "--no-cpu-baseline", "--no-config4", "--dump-records", dump, *extra]
+    p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_gather_equals_one_process(tmp_path):
+    two = _bench(2, str(tmp_path / "two.npy"))
+    one = _bench(1, str(tmp_path / "one.npy"))
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    r = two["ranks"]
+    assert r["world_size_observed"] == 2 and r["backend"] == "gloo" and len(r["rank_seconds"]) == 2
+    assert sorted(r["shard_objects"]) == [4, 4] and r["gather_ms_per_step"] > 0
+    assert two["config"]["objects"] == one["config"]["objects"] == 8
+    a, b = np.load(tmp_path / "two.npy"), np.load(tmp_path / "one.npy")
+    assert a.shape == b.shape == (8, 83)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (a[:, 1] == 1).all()
+    assert two["lite_broken_blocks"] == 0 == one["lite_broken_blocks"]

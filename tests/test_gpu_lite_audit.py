@@ -10,7 +10,7 @@ any of them discards that object's iteration and redoes it, and the rest of the 
 with every sample decoded exactly (k_solve, k_iter_begin).
 
 These tests (1) force violations with a deterministic perturbation of every lite value
-(DSR_LITE_PERTURB) and show the guard fires and the results equal exact decoding
+(DSR_LITE_PERTURB, a test hook the library honours only under DSR_TEST_HOOKS=1) and show the guard fires and the results equal exact decoding
 (DSR_LITE=0) at the teacher-forced tolerances; (2) check later iterations — where the
 margin has calibrated down to max(0.002, 4 x the observed error) — against exact decoding from the same
 state, on the bench decoder and on a decoder with larger hidden weights (larger
@@ -89,7 +89,9 @@ def test_audit_guard_fires_and_redoes_exactly(gpu_decoder, monkeypatch):
     # (th + m, first-iteration margin m = 0.01) all land in the audit shell th+m..th+2m, so
     # every object sees violations
     monkeypatch.setenv("DSR_LITE_PERTURB", "0.015")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
     outs, st = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert st.test_hooks == 1
     assert st.lite == 1 and st.audit_points > 0
     assert st.lite_audit_violations > 0
     assert st.lite_redo_objects == len(objs)
@@ -111,6 +113,8 @@ def test_audit_quiet_and_cheap_on_the_bench_workload(gpu_decoder, monkeypatch):
     objs = [S.kitti_object(i) for i in range(8)]
     outs, st = batch_stats(opt, [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
     assert st.lite_audit_violations == 0 and st.lite_redo_objects == 0
+    # the default staggered kernel never hit a bounded event wait
+    assert st.lite_broken_blocks == 0 and st.test_hooks == 0
     assert st.audit_points > 0
     assert st.audit_points <= 0.1 * st.fwd_points, (st.audit_points, st.fwd_points)
     # margin = max(0.002, 4 x the object's largest observed error), well inside th = 0.01
@@ -144,3 +148,138 @@ def test_calibrated_margin_iterations_match_exact(gain, monkeypatch):
         monkeypatch.setenv("DSR_LITE", "1")
         for j, e in enumerate((1, 2, 3)):
             assert_same_step(tr[i], t0[j], e1=e, e0=0, what=f"gain {gain} object {i} iteration {e}")
+
+
+def test_test_hooks_ignored_without_the_gate(gpu_decoder, monkeypatch):
+    """DSR_LITE_PERTURB / DSR_LITE_BREAK change nothing unless DSR_TEST_HOOKS=1 (a stray
+    variable cannot alter a production run), and dsr_stats reports the gate."""
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=1)
+    objs = [(f["it_t_obj_cam"][0], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][0])]
+    monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.delenv("DSR_TEST_HOOKS", raising=False)
+    ref, st0 = batch_stats(opt, objs, pose_is_obj_cam=True)
+    monkeypatch.setenv("DSR_LITE_PERTURB", "0.015")
+    monkeypatch.setenv("DSR_LITE_BREAK", "1")
+    outs, st = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert st.test_hooks == 0 and st0.test_hooks == 0
+    assert st.lite_audit_violations == 0 and st.lite_broken_blocks == 0
+    assert st.refine_points == st0.refine_points < st.fwd_points
+    assert bytes(outs) == bytes(ref)
+
+
+def _violating_batch(opt, objs, monkeypatch):
+    """A resident batch whose every object sees audit violations (DSR_LITE_PERTURB)."""
+    from reconstruct import _libdsr as L
+
+    monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
+    monkeypatch.setenv("DSR_LITE_PERTURB", "0.015")
+    keep = []
+    ins = (L.ObjectIn * len(objs))()
+    for i, ob in enumerate(objs):
+        ins[i] = opt._object_in(*ob[:4], ob[4], keep, True)
+    ctx = opt._ctx
+    h = C.c_void_p()
+    ctx.check(ctx.lib.dsr_batch_create(ctx.handle, opt.decoder.handle, C.byref(opt.params), len(objs), ins,
+                                       C.byref(h)), "create")
+    return h, keep
+
+
+def test_graph_replays_redo_the_spare_iteration(gpu_decoder, monkeypatch):
+    """DSR_GRAPH=1 re-runs replay the captured regular iterations; a run whose audit discards
+    an iteration still gets its spare iteration on every replay (the spare flag
+    was left set by the previous run, so replays 3.. skipped it and reported is_good=0)."""
+    from reconstruct import _libdsr as L
+
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=2)
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e]) for e in (0, 4)]
+    monkeypatch.setenv("DSR_GRAPH", "1")
+    h, keep = _violating_batch(opt, objs, monkeypatch)
+    ctx = opt._ctx
+    runs = []
+    try:
+        for _ in range(3):
+            outs = (L.ObjectOut * len(objs))()
+            ctx.check(ctx.lib.dsr_batch_run(h), "run")
+            ctx.check(ctx.lib.dsr_batch_download(h, outs), "download")
+            st = L.Stats()
+            ctx.check(ctx.lib.dsr_batch_stats(h, C.byref(st)), "stats")
+            assert st.lite_redo_objects == len(objs)
+            for o in outs:
+                assert o.is_good == 1 and o.iters_done == 2, (o.is_good, o.iters_done, o.fail_reason)
+            runs.append(bytes(outs))
+    finally:
+        ctx.lib.dsr_batch_destroy(h)
+    assert runs[0] == runs[1] == runs[2]
+
+
+def test_audit_setting_is_fixed_at_batch_creation(gpu_decoder, monkeypatch):
+    """A batch created with DSR_LITE_AUDIT=0 has no spare iteration; turning the variable on
+    before a run must not switch the audit on for that batch (it did, a violation
+    then discarded an iteration with no spare to redo it and the object came back failed)."""
+    from reconstruct import _libdsr as L
+
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=1)
+    objs = [(f["it_t_obj_cam"][0], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][0])]
+    monkeypatch.setenv("DSR_LITE_AUDIT", "0")
+    h, keep = _violating_batch(opt, objs, monkeypatch)
+    ctx = opt._ctx
+    try:
+        monkeypatch.setenv("DSR_LITE_AUDIT", "1")
+        outs = (L.ObjectOut * 1)()
+        ctx.check(ctx.lib.dsr_batch_run(h), "run")
+        ctx.check(ctx.lib.dsr_batch_download(h, outs), "download")
+        st = L.Stats()
+        ctx.check(ctx.lib.dsr_batch_stats(h, C.byref(st)), "stats")
+    finally:
+        ctx.lib.dsr_batch_destroy(h)
+    assert st.lite_audit_violations == 0 and st.audit_points == 0
+    assert outs[0].is_good == 1 and outs[0].iters_done == 1
+
+
+def test_query_never_waits_for_the_redo(gpu_decoder, monkeypatch):
+    """dsr_batch_query enqueues a pending audit redo and reports the batch as still in flight
+    instead of waiting for it (the async keyframe API's overlap); polling to completion gives
+    the synchronous result.  A batch captured as a graph but never run cannot be queried."""
+    import time
+
+    from reconstruct import _libdsr as L
+
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=1)
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e]) for e in (0, 4)]
+    h, keep = _violating_batch(opt, objs, monkeypatch)
+    ctx = opt._ctx
+    lib = ctx.lib
+    try:
+        ctx.check(lib.dsr_batch_run(h), "run")
+        seen, slow = [], 0.0
+        for _ in range(100000):
+            t0 = time.perf_counter()
+            rc = lib.dsr_batch_query(h)
+            slow = max(slow, time.perf_counter() - t0)
+            assert rc >= 0
+            seen.append(rc)
+            if rc == 1:
+                break
+        assert seen[-1] == 1
+        polled = (L.ObjectOut * 2)()
+        ctx.check(lib.dsr_batch_download(h, polled), "download")
+        ctx.check(lib.dsr_batch_run(h), "run")
+        synced = (L.ObjectOut * 2)()
+        ctx.check(lib.dsr_batch_download(h, synced), "download")
+        assert bytes(polled) == bytes(synced)
+        assert all(o.is_good == 1 and o.iters_done == 1 for o in polled)
+        print(f"\nlongest query {slow * 1e3:.3f} ms over {len(seen)} polls")
+    finally:
+        lib.dsr_batch_destroy(h)
+    monkeypatch.setenv("DSR_GRAPH", "1")
+    h, keep = _violating_batch(opt, objs, monkeypatch)
+    try:
+        ctx.check(lib.dsr_batch_graph(h), "graph")
+        assert lib.dsr_batch_query(h) < 0          # captured, never run
+    finally:
+        lib.dsr_batch_destroy(h)

@@ -648,6 +648,7 @@ def test_lite_broken_block_falls_back_to_exact(gpu_decoder, monkeypatch):
 
     lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
     sig = {}
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
     for mode in ("exact", "broken"):
         monkeypatch.setenv("DSR_LITE", "0" if mode == "exact" else "1")
         monkeypatch.setenv("DSR_LITE_BREAK", "1" if mode == "broken" else "0")
@@ -661,6 +662,8 @@ def test_lite_broken_block_falls_back_to_exact(gpu_decoder, monkeypatch):
             rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
                            np.float32)
             sig[mode] = (rec, st.jac_points, st.refine_points, st.fwd_points)
+            if mode == "broken":      # every started block counted as broken (dsr_stats)
+                assert st.test_hooks == 1 and st.lite_broken_blocks > 0
         finally:
             lib.dsr_batch_destroy(h)
     assert np.array_equal(sig["broken"][0].view(np.uint32), sig["exact"][0].view(np.uint32))

@@ -6,7 +6,7 @@
   is covered by tests/test_gpu_api.py::test_entry_path_as_the_cpp_side_calls_it;
 * argument validation before anything reaches C (a short code would be an
   out-of-bounds read there: the ABI copies code_len floats);
-* the ingest hook resolves only the four named data-ingest modules;
+* the ingest hook runs the reference's own data-ingest modules (and resolves nothing else);
 * golden F9 (tests/golden/make_mesher.py): the reference's voxel grid and its vertex
   transform around marching cubes.
 """
@@ -83,21 +83,87 @@ def test_short_code_is_rejected_before_c():
         mex.extract_mesh_from_code(short)
 
 
-def test_ingest_hook_resolves_only_named_modules(tmp_path, monkeypatch):
-    import reconstruct
-    from reconstruct.utils import ForceKeyErrorDict
+REF_RECONSTRUCT = "/root/reference/reconstruct"
 
-    (tmp_path / "mono_sequence.py").write_text(
-        "class MonoSequence:\n    def __init__(self, d, c):\n        self.d = d\n")
-    (tmp_path / "loss.py").write_text("raise RuntimeError('must never be imported')\n")
-    monkeypatch.setenv("DSR_REFERENCE_RECONSTRUCT", str(tmp_path))
-    monkeypatch.delitem(sys.modules, "reconstruct.mono_sequence", raising=False)
-    seq = reconstruct.get_sequence("/data", ForceKeyErrorDict(data_type="Redwood"))
-    assert seq.d == "/data"
+
+class _CV2Stub:
+    """cv2 is absent here; the reference's ingest modules need it only inside frames
+    (imread, undistortPoints) and for MonoSequence's intrinsics (FileStorage)."""
+
+    FILE_STORAGE_READ = 0
+
+    class FileStorage:
+        VALUES = {"Camera.fx": 525.0, "Camera.fy": 520.0, "Camera.cx": 319.5, "Camera.cy": 239.5,
+                  "Camera.k1": 0.01, "Camera.k2": -0.02}
+
+        def __init__(self, path, mode):
+            self.path = path
+
+        def getNode(self, key):
+            v = self.VALUES[key]
+            return type("Node", (), {"real": lambda self: v})()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_RECONSTRUCT), reason="reference tree not present (GPU box)")
+def test_ingest_hook_runs_the_reference_modules(tmp_path, monkeypatch):
+    """System.cc:99 calls reconstruct.get_sequence at every start-up.  Through the ingest hook
+    the build loads the reference's OWN kitti_sequence.py / mono_sequence.py, which import
+    get_rays / get_time from reconstruct.loss_utils and read_calib_file / load_velo_scan /
+    ForceKeyErrorDict from reconstruct.utils (kitti_sequence.py:22-24, mono_sequence.py:22-24):
+    both sequences construct, calibration parsed by this package's reader.  Nothing else
+    resolves to the reference: reconstruct.loss stays an ImportError although the directory
+    holds loss.py."""
+    import types
+
+    import reconstruct
+    from reconstruct.loss_utils import get_rays
+    from reconstruct.utils import ForceKeyErrorDict, load_velo_scan, read_calib_file
+
+    cv2 = types.ModuleType("cv2")
+    for k, v in vars(_CV2Stub).items():
+        if not k.startswith("__"):
+            setattr(cv2, k, v)
+    monkeypatch.setitem(sys.modules, "cv2", cv2)
+    monkeypatch.setenv("DSR_REFERENCE_RECONSTRUCT", REF_RECONSTRUCT)
+    for name in ("kitti_sequence", "mono_sequence"):
+        monkeypatch.delitem(sys.modules, "reconstruct." + name, raising=False)
+    # a KITTI sequence directory: calib.txt (P2 with a baseline term, Tr), two images, a scan
+    d = tmp_path / "seq"
+    (d / "image_2").mkdir(parents=True)
+    for k in range(2):
+        (d / "image_2" / f"{k:06d}.png").write_bytes(b"")
+    P2 = [721.5, 0, 609.6, 44.9, 0, 721.5, 172.9, 0.2, 0, 0, 1, 0.003]
+    Tr = [0.0, -1, 0, 0.01, 0, 0, -1, -0.07, 1, 0, 0, -0.27]
+    (d / "calib.txt").write_text("P0: " + " ".join(map(str, P2)) + "\nP2: " + " ".join(map(str, P2))
+                                 + "\nTr: " + " ".join(map(str, Tr)) + "\ndate: 2011-09-26\n\nP3: 1 2\n")
+    cal = read_calib_file(str(d / "calib.txt"))
+    assert set(cal) == {"P0", "P2", "Tr"} and cal["P2"].dtype == np.float64
+    cfg = ForceKeyErrorDict(data_type="KITTI", detect_online=False, path_label_2d=str(tmp_path / "l2"),
+                            path_label_3d=str(tmp_path / "l3"))
+    seq = reconstruct.get_sequence(str(d), cfg)
+    assert type(seq).__name__ == "KITIISequence" and seq.num_frames == 2
+    K = np.array(P2, np.float64).reshape(3, 4)[:, :3]
+    assert np.allclose(seq.K_cam, K) and np.allclose(seq.invK_cam, np.linalg.inv(K), rtol=1e-6)
+    assert np.isclose(seq.T_cam_velo[0, 3], Tr[3] + P2[3] / P2[0], rtol=1e-6)
+    assert seq.detector_2d is None and seq.detector_3d is None
+    # the rays the reference's frames build with this package's get_rays (kitti_sequence.py:209)
+    px = np.array([[100.0, 50.0], [600.5, 180.25]])
+    rays = get_rays(px, seq.invK_cam)
+    assert rays.dtype == np.float32
+    assert np.allclose(rays, (np.c_[px, np.ones(2)] @ seq.invK_cam.T), rtol=1e-6)
+    scan = np.arange(12, dtype=np.float32)
+    scan.tofile(str(d / "scan.bin"))
+    assert np.array_equal(load_velo_scan(str(d / "scan.bin")), scan.reshape(3, 4))
+    # a Redwood (mono) sequence: intrinsics through cv2.FileStorage
+    mcfg = ForceKeyErrorDict(data_type="Redwood", detect_online=False, slam_config_path="x.yaml",
+                             path_label_2d=str(tmp_path / "l2"))
+    mono = reconstruct.get_sequence(str(tmp_path), mcfg)
+    assert type(mono).__name__ == "MonoSequence" and mono.K_cam[0, 0] == 525.0 and mono.k2 == -0.02
     with pytest.raises(ImportError):
         import reconstruct.loss  # noqa: F401
     assert reconstruct.get_detectors(ForceKeyErrorDict(detect_online=False, data_type="KITTI")) == (None, None)
-    monkeypatch.delitem(sys.modules, "reconstruct.mono_sequence", raising=False)
+    for name in ("kitti_sequence", "mono_sequence"):
+        monkeypatch.delitem(sys.modules, "reconstruct." + name, raising=False)
 
 
 def test_voxel_grid_matches_reference_f9():

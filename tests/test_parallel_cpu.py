@@ -75,6 +75,154 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+class _FakeLib:
+    """Stands in for libdsr's resident-batch entry points on CPU (test infrastructure): the
+    batch keeps the objects dsr_batch_create received through the C structs and a run solves
+    them with the CPU oracle, so ResidentShard's partition, upload, download, record packing
+    and gather run exactly as on the GPU."""
+
+    def __init__(self):
+        self.batches = {}
+        self.solve = _solver()
+
+    def dsr_batch_create(self, ctx, dec, params, n, ins, hout):
+        objs = []
+        for k in range(n):
+            r = ins[k]
+            arr = lambda p, m: np.ctypeslib.as_array(p, shape=(m,)).copy()  # noqa: E731
+            objs.append((np.array(r.t_cam_obj, np.float32).reshape(4, 4),
+                         arr(r.pts, 3 * r.n_pts).reshape(-1, 3), arr(r.rays, 3 * r.n_rays).reshape(-1, 3),
+                         arr(r.depth, r.n_depth), None))
+        key = len(self.batches) + 1
+        self.batches[key] = {"objs": objs, "res": None}
+        hout._obj.value = key
+        return 0
+
+    def dsr_batch_run(self, h):
+        b = self.batches[h.value]
+        b["res"] = self.solve(b["objs"])
+        return 0
+
+    def dsr_batch_download(self, h, outs):
+        for k, r in enumerate(self.batches[h.value]["res"]):
+            o = outs[k]
+            o.is_good = int(r["is_good"])
+            o.loss = float(r["loss"])
+            o.iters_done = int(r["iters_done"])
+            if r["is_good"]:
+                o.t_cam_obj[:] = np.asarray(r["t_cam_obj"], np.float32).reshape(-1).tolist()
+                o.code[:] = np.asarray(r["code"], np.float32).tolist()
+        return 0
+
+    def dsr_batch_destroy(self, h):
+        self.batches.pop(h.value, None)
+        return 0
+
+
+def _fake_optimizer():
+    import ctypes
+
+    import synthetic as S
+    from reconstruct.optimizer import Optimizer
+    from reconstruct.utils import ForceKeyErrorDict
+
+    class Ctx:
+        lib = _FakeLib()
+        handle = ctypes.c_void_p(1)
+
+        def check(self, rc, what):
+            assert rc == 0, what
+
+    class Dec:
+        ctx = Ctx()
+        handle = ctypes.c_void_p(2)
+
+    cfg = ForceKeyErrorDict(data_type="Redwood", optimizer=dict(
+        S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"], num_iterations=1)))
+    return Optimizer(Dec(), cfg)
+
+
+def _resident_worker(rank, world, port, q):
+    import sys
+
+    for p in (PKG, REPO):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from reconstruct.parallel import ResidentShard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shard = ResidentShard(_fake_optimizer(), _objects())
+        first = shard.run()
+        second = shard.run()                 # inputs stay resident: a re-run gives the same records
+        if rank == 0:
+            q.put({"mine": shard.mine, "shards": shard.shards, "gather": shard.last_gather_s,
+                   "res": [(r["is_good"], r["loss"], None if r["t_cam_obj"] is None else r["t_cam_obj"].tolist(),
+                            r["iters_done"]) for r in first],
+                   "same": all(a["loss"] == b["loss"] for a, b in zip(first, second))})
+        else:
+            assert first is None and second is None
+        shard.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_resident_shard_world2_equals_one_process():
+    """bench.py's N>1 path (reconstruct/parallel.py: ResidentShard): each of 2 gloo ranks
+    uploads only its LPT shard, runs it, and one all-gather returns every object's record to
+    rank 0 in input order — equal to the one-process ResidentShard."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resident_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from reconstruct.parallel import ResidentShard
+
+    one = ResidentShard(_fake_optimizer(), _objects())
+    ref = one.run()
+    assert sorted(i for s in got["shards"] for i in s) == list(range(len(ref)))
+    assert all(len(s) > 0 for s in got["shards"]) and got["gather"] > 0.0 and got["same"]
+    for (good, loss, T, it), r in zip(got["res"], ref):
+        assert good == r["is_good"] and it == r["iters_done"]
+        assert np.float32(loss) == np.float32(r["loss"])
+        if good:
+            assert np.array_equal(np.asarray(T, np.float32), np.asarray(r["t_cam_obj"], np.float32))
+
+
+def test_bench_spawns_its_own_ranks(monkeypatch):
+    """`python bench.py --gpus N` without a launcher starts torch.distributed.run with N local
+    ranks as a child process (no exec of a process that touched the GPU)."""
+    import subprocess
+    import sys
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    calls = []
+    monkeypatch.setattr(subprocess, "call", lambda cmd: calls.append(cmd) or 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+    (cmd,) = calls
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"]
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.main()
+
+
 def test_lpt_partition_balances_and_covers():
     from reconstruct.parallel import lpt_partition
 
