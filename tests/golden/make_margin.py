@@ -302,6 +302,7 @@ def main():
 
     redwood = lambda s: S.make_object(s, n_pts=512, scale=1.0, tz=3.0, upright=False)  # noqa: E731
     kitti = lambda s: tilted(S.make_object(s, n_pts=2048, scale=2.0, tz=15.0, upright=True), s)  # noqa
+    kitti512 = lambda s: tilted(S.make_object(s, n_pts=512, scale=2.0, tz=15.0, upright=True), s)  # noqa
     families = [
         # (tag, optim, data_type, object factory(seed), n_fg, n_bg, wanted, max tries)
         ("redwood", S.REDWOOD_OPTIM, "Redwood", redwood, 32, 8, 2, 400),
@@ -311,6 +312,14 @@ def main():
         # are reproducible to the contract where the full iteration counts found none
         ("redwood3it", iters(S.REDWOOD_OPTIM, 3), "Redwood", redwood, 32, 8, 2, 200),
         ("kitti3it", iters(S.KITTI_OPTIM, 3), "KITTI", kitti, 32, 8, 2, 200),
+        # round 3: KITTI parameters (upright prior k4 = 1e7 active: the tilted start keeps
+        # res_rot > 1e-7, its fp32 rounding boundary recorded as margin_rot_ulps) with 2 GN
+        # iterations — 3 found none whose 8-member ensemble stayed within the contract (the
+        # code spreads 1e-3..1e-2 through the Jacobian points' ReLU kinks, amplified by the
+        # weakly regularised code block of H: k3 = 0.25); ~2% of 2-iteration inputs qualify
+        ("kitti2it", iters(S.KITTI_OPTIM, 2), "KITTI", kitti, 32, 8, 3, 200),
+        ("kitti2it_r64", iters(S.KITTI_OPTIM, 2), "KITTI", kitti, 64, 8, 2, 200),
+        ("kitti2it_p512", iters(S.KITTI_OPTIM, 2), "KITTI", kitti512, 32, 8, 2, 200),
     ]
     if args.family:
         families = [f for f in families if f[0] in args.family.split(",")]

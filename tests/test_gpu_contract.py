@@ -17,12 +17,11 @@ is checked two ways:
   reference's result: identical K every
   iteration, final pose (rotation·scale block and translation, max-norm relative) and
   code <= 1e-3, loss <= 1e-4, on both decode paths (DSR_LITE=1 default, DSR_LITE=0);
-* by envelope, on the full-size bench objects (F4): the build's deviation from the
-  reference's 1-thread result is no larger than twice the largest deviation among the
-  members of the reference's own ensemble (64 runs at 1 thread with the initial pose
-  perturbed by one fp32 ulp, tests/golden/make_ensemble.py, plus runs at 2/4/8 threads),
-  or the contract tolerance where that is larger — i.e. the GPU result is one more member of the reference's own
-  reproducibility cloud, for pose, code and loss alike.
+* by ensemble, on the full-size bench objects (F4, the metric configuration): the GPU runs
+  the same 64 initial poses, each perturbed by one fp32 ulp, that the reference's own
+  ensemble ran (tests/golden/make_ensemble.py), and the two output distributions — final
+  loss, code and pose — must agree (means, Kolmogorov-Smirnov, medians): the GPU is the
+  reference's reproducibility cloud, not one lucky member of it.
 
 The CPU oracle is held to the strict contract on the same F8 fixtures in
 ``tests/test_oracle_golden.py::test_oracle_final_state_on_margin_fixtures``.
@@ -128,22 +127,62 @@ def test_every_iteration_state_tracks_reference(gpu_decoder, path):
         assert e_loss <= (LOSS_TOL if e == n_it - 1 else POSE_TOL), e
 
 
-@pytest.mark.parametrize("name,optim,dtp", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),
-                                            ("redwood1", S.REDWOOD_OPTIM, "Redwood"),
-                                            ("kitti0", S.KITTI_OPTIM, "KITTI"),
-                                            ("kitti5", S.KITTI_OPTIM, "KITTI")])
-def test_full_size_final_state_within_reference_envelope(gpu_decoder, name, optim, dtp):
+ENS = "ens64_"
+
+
+def _ks_p(a, b):
+    from scipy.stats import ks_2samp
+
+    return float(ks_2samp(a, b).pvalue)
+
+
+@pytest.mark.parametrize("name,optim,dtp", [("kitti0", S.KITTI_OPTIM, "KITTI"),
+                                            ("kitti5", S.KITTI_OPTIM, "KITTI"),
+                                            ("redwood0", S.REDWOOD_OPTIM, "Redwood"),
+                                            ("redwood1", S.REDWOOD_OPTIM, "Redwood")])
+def test_full_size_ensemble_matches_reference_ensemble(gpu_decoder, name, optim, dtp):
+    """At the metric configuration (F4: KITTI 2048 pts x 2248 rays x 10 iterations; Redwood
+    512 x 712 x 5) the reference does not reproduce itself to the contract: one fp32 ulp on
+    the initial pose moves its final code by up to 5.6e-1.  So the GPU runs the
+    SAME 64 ulp-perturbed initial poses the reference's ensemble ran (tests/golden/
+    make_ensemble.py: ens64_t_init) and the two output distributions are compared:
+
+    * final loss: the ensemble means agree within 3 standard errors of their difference,
+      3·sqrt(σ_ref² + σ_gpu²)/√64 (a systematic bias shows here; the max-envelope of round 2
+      could not see one);
+    * final loss, code and pose deviations from the reference's unperturbed result: the two
+      samples are not distinguishable (two-sample Kolmogorov-Smirnov p >= 1e-3) and their
+      medians agree within a factor 2;
+    * every member converges (is_good) in both.
+    Reference: optimizer.py:90-205 as run by the ensemble generator, 1 CPU thread per member."""
     f = golden(f"f4_traj_{name}.npz")
-    r, _ = _run(gpu_decoder, f, optim, dtp)
-    assert r["is_good"]
-    gpu = np.array(contract_errors(r["t_cam_obj"], r["code"], r["loss"], f))
-    # every member the fixture holds: 64 (or 16) 1-thread ulp-perturbed runs, plus the 2/4/8
-    # thread runs (a perturbation at every reduction, like the GPU's own summation order)
-    keys = [k for k in ("ens64_", "ens16_") if k + "loss" in f.files][:1] + ["ens_"]
-    ens = np.array([contract_errors(f[k + "t_cam_obj"][m], f[k + "code"][m], f[k + "loss"][m], f)
-                    for k in keys for m in range(len(f[k + "loss"]))])
-    env = np.nanmax(ens, axis=0)
-    tol = np.maximum([POSE_TOL, POSE_TOL, CODE_TOL, LOSS_TOL], 2.0 * env)
-    print(f"\n{name}: gpu rot/t/code/loss {np.array2string(gpu, precision=2)} reference ensemble "
-          f"{np.array2string(env, precision=2)}")
-    assert (gpu <= tol).all(), (gpu, env)
+    t_init = f[ENS + "t_init"]
+    n = t_init.shape[0]
+    from reconstruct.optimizer import Optimizer
+
+    opt = Optimizer(gpu_decoder, make_cfg(optim, dtp))
+    res = opt.reconstruct_objects([(t_init[m], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)
+                                   for m in range(n)])
+    assert all(r["is_good"] for r in res) and bool(np.all(f[ENS + "is_good"]))
+    g_loss = np.array([r["loss"] for r in res], np.float64)
+    r_loss = f[ENS + "loss"].astype(np.float64)
+    se = np.sqrt((r_loss.var(ddof=1) + g_loss.var(ddof=1)) / n)
+    d_mean = abs(g_loss.mean() - r_loss.mean())
+    g_err = np.array([contract_errors(r["t_cam_obj"], r["code"], r["loss"], f) for r in res])
+    r_err = np.array([contract_errors(f[ENS + "t_cam_obj"][m], f[ENS + "code"][m], f[ENS + "loss"][m], f)
+                      for m in range(n)])
+    cols = ("rot", "t", "code")
+    p = {c: _ks_p(g_err[:, k], r_err[:, k]) for k, c in enumerate(cols)}
+    p["loss"] = _ks_p(g_loss, r_loss)
+    med = {c: float(np.median(g_err[:, k]) / max(np.median(r_err[:, k]), 1e-30)) for k, c in enumerate(cols)}
+    q = lambda a: np.array2string(np.quantile(a, [0.1, 0.5, 0.9]), precision=2)  # noqa: E731
+    print(f"\n{name}: loss mean gpu {g_loss.mean():.6f} ref {r_loss.mean():.6f} (|d| {d_mean:.2e}, "
+          f"3 SE {3 * se:.2e}; one-sample 3σ_ref/√n {3 * r_loss.std(ddof=1) / np.sqrt(n):.2e}) "
+          f"σ gpu {g_loss.std(ddof=1):.2e} ref {r_loss.std(ddof=1):.2e}")
+    for k, c in enumerate(cols):
+        print(f"  {c}: deviation quantiles 10/50/90% gpu {q(g_err[:, k])} ref {q(r_err[:, k])} "
+              f"KS p {p[c]:.3f} median ratio {med[c]:.2f}")
+    print(f"  loss quantiles gpu {q(g_loss)} ref {q(r_loss)} KS p {p['loss']:.3f}")
+    assert d_mean <= 3 * se, (d_mean, se)
+    assert min(p.values()) >= 1e-3, p
+    assert all(0.5 <= v <= 2.0 for v in med.values()), med

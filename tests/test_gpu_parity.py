@@ -603,9 +603,13 @@ def test_refine_stops_at_ray_termination(gpu_decoder, monkeypatch):
 
 @pytest.mark.gpu
 def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
-    """The staggered-group lite kernel (DSR_LITE_VARIANT=216: LDS event counters instead of
-    block barriers, dsr_mlp_lite.hpp: k_mlp_fwd_lite_st) runs the same MFMAs in the same k
-    order as the barrier kernel (88): results bitwise equal, for several stagger lags."""
+    """The staggered-group lite kernel (default DSR_LITE_VARIANT=1496: LDS event counters
+    instead of block barriers, dsr_mlp_lite.hpp: k_mlp_fwd_lite_st) gives the same lite values
+    whatever the stagger lag (0: B may start each GEMM at once, 7: half a GEMM behind) — a
+    race on the LDS image would change values, classes and counts — and equals the unswizzled
+    variant 472 bitwise; no block's bounded event wait expires (dsr_stats.lite_broken_blocks).
+    (Round 2 tested the scaled-epilogue variant 216 against the barrier kernel 88 here; 216
+    is no longer in the shipped library)"""
     import ctypes
 
     import bench
@@ -614,7 +618,7 @@ def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
     lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
     monkeypatch.setenv("DSR_LITE", "1")
     sig = {}
-    for v, lag in (("88", "4"), ("216", "0"), ("216", "4"), ("216", "7")):
+    for v, lag in (("1496", "4"), ("1496", "0"), ("1496", "7"), ("472", "4")):
         monkeypatch.setenv("DSR_LITE_VARIANT", v)
         monkeypatch.setenv("DSR_LITE_LAG", lag)
         h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
@@ -627,9 +631,10 @@ def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
             rec = np.array([list(o.t_cam_obj) + list(o.code) + [o.loss, o.is_good, o.iters_done] for o in outs],
                            np.float32)
             sig[(v, lag)] = (rec, st.fwd_points, st.refine_points, st.jac_points)
+            assert st.lite_broken_blocks == 0, (v, lag, L.lite_diag(lib, h))
         finally:
             lib.dsr_batch_destroy(h)
-    ref = sig[("88", "4")]
+    ref = sig[("1496", "4")]
     for k, s in sig.items():
         assert np.array_equal(s[0].view(np.uint32), ref[0].view(np.uint32)), k
         assert s[1:] == ref[1:], k

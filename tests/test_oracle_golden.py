@@ -195,3 +195,25 @@ def test_oracle_final_state_on_margin_fixtures(oracle_dec, path):
     e_rot, e_t, e_z, e_l = contract_errors(r.t_cam_obj, r.code, r.loss, f)
     assert e_rot <= POSE_TOL and e_t <= POSE_TOL and e_z <= CODE_TOL and e_l <= LOSS_TOL, \
         (e_rot, e_t, e_z, e_l)
+
+
+def test_kitti_margin_fixtures_run_the_rotation_prior():
+    """The strict contract covers KITTI parameters (configs/config_kitti.json: upright prior
+    k4 = 1e7) with the prior ACTIVE: at every iteration of every KITTI F8 fixture the
+    reference's res_rot = 1 - (R_co e_y).(0,-1,0) (loss.py:169-192) is far above its 1e-7
+    switch, and the fp32 switch decision keeps a recorded margin of >= 4 ulps."""
+    from test_gpu_contract import optim_of
+
+    paths = [p for p in _f8_paths() if str(np.load(p)["data_type"]) == "KITTI"]
+    assert len(paths) >= 3
+    for p in paths:
+        f = np.load(p, allow_pickle=False)
+        optim, _ = optim_of(f)
+        assert optim["joint_optim"]["k4"] == 1e7
+        n_it = int(f["n_iters_run"])
+        assert n_it >= 2 and f["is_good"]
+        for e in range(n_it):
+            tco = np.linalg.inv(f["it_t_obj_cam"][e].astype(np.float64))
+            r = tco[:3, :3] / np.cbrt(np.linalg.det(tco[:3, :3]))
+            assert 1.0 + r[1, 1] > 1e-6, (p, e)
+        assert (f["margin_rot_ulps"][:n_it] >= 4.0).all()

@@ -23,7 +23,7 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS)
 lib, ctx = dec.ctx.lib, dec.ctx
 os.environ["DSR_LITE"] = "1"
-for v, lag in (("88", "4"), ("216", "0"), ("216", "4"), ("1496", "4")):
+for v, lag in (("88", "4"), ("472", "4"), ("1496", "0"), ("1496", "4")):
     os.environ["DSR_LITE_VARIANT"] = v
     os.environ["DSR_LITE_LAG"] = lag
     for r in range(reps):

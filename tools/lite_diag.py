@@ -28,8 +28,10 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS)
 lib, ctx = dec.ctx.lib, dec.ctx
 os.environ["DSR_LITE"] = "1"
-configs = [("1496", "4", "4"), ("216", "0", "4"), ("216", "4", "4"), ("216", "0", "2"), ("216", "0", "1"),
-           ("1496", "4", "2")]
+# (216 needs a -DDSR_LITE_EXPERIMENTS build: DSR_LIB=<that .so> DSR_DIAG_216=1)
+configs = [("1496", "4", "4"), ("1496", "0", "4"), ("1496", "4", "2"), ("472", "4", "4")]
+if os.environ.get("DSR_DIAG_216") == "1":
+    configs += [("216", "0", "4"), ("216", "4", "4"), ("216", "0", "2"), ("216", "0", "1")]
 for v, lag, streams in configs:
     os.environ.update(DSR_LITE_VARIANT=v, DSR_LITE_LAG=lag, DSR_STREAMS=streams)
     for r in range(reps):
