@@ -347,7 +347,9 @@ def main():
     backend = os.environ.get("DSR_BENCH_BACKEND", "nccl")
     import torch
 
-    if world > 1:
+    # DSR_BENCH_FORCE_DIST=1: initialise the process group even for one rank, so a one-GPU box
+    # runs the N>1 code path (RCCL collectives on device tensors) end to end
+    if world > 1 or os.environ.get("DSR_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
 
         if backend == "nccl":
@@ -356,7 +358,7 @@ def main():
         else:
             dist.init_process_group(backend)
             local = local % max(1, torch.cuda.device_count())
-    coll_dev = torch.device("cuda", local) if backend == "nccl" and world > 1 else None
+    coll_dev = torch.device("cuda", local) if backend == "nccl" and dist is not None else None
 
     from deep_sdf.workspace import decoder_from_state
     from reconstruct import _libdsr as L

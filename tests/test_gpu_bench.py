@@ -24,11 +24,14 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-def _bench(n, dump, extra=()):
+ARGS = ["--steps", "1", "--warmup", "0", "--objects", "8", "--no-extra", "--no-cpu-baseline", "--no-config4"]
+
+
+def _bench(n, dump, extra=(), env_extra=None, launcher=()):
     env = dict(os.environ, DSR_BENCH_BACKEND="gloo")
+    env.update(env_extra or {})
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0", "--objects", "8",
-           "--no-extra", "--no-cpu-baseline", "--no-config4", "--dump-records", dump, *extra]
+    cmd = [sys.executable, *launcher, "bench.py", "--gpus", str(n), *ARGS, "--dump-records", dump, *extra]
     p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])
@@ -48,3 +51,27 @@ def test_bench_two_ranks_gather_equals_one_process(tmp_path):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert (a[:, 1] == 1).all()
     assert two["lite_broken_blocks"] == 0 == one["lite_broken_blocks"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_rccl_path_on_one_rank(tmp_path):
+    """The driver's N>1 runs go through torch.distributed.run with backend "nccl" (RCCL over
+    xGMI), which needs one GPU per rank.  On this one-GPU box the same code path runs with one
+    rank (DSR_BENCH_FORCE_DIST=1): RCCL process group, device-tensor all-gather of the records,
+    barrier and max-over-ranks timing — records bitwise those of the plain one-process run."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    launcher = ("-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr", "127.0.0.1",
+                "--master-port", str(port))
+    rccl = _bench(1, str(tmp_path / "rccl.npy"), env_extra={"DSR_BENCH_FORCE_DIST": "1", "DSR_BENCH_BACKEND": "nccl"},
+                  launcher=launcher)
+    one = _bench(1, str(tmp_path / "one.npy"))
+    r = rccl["ranks"]
+    assert r["backend"] == "nccl" and r["world_size_observed"] == 1 and r["gather_ms_per_step"] > 0
+    assert "backend" not in one["ranks"]
+    a, b = np.load(tmp_path / "rccl.npy"), np.load(tmp_path / "one.npy")
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
