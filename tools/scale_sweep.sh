@@ -11,11 +11,11 @@ run() {   # name, env..., -- bench args
   echo "$name rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
-run o64 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-extra --no-cpu-baseline
-run o8g DSR_GRAPH=1 timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-extra --no-cpu-baseline --objects 8
-run o16 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --objects 16
-run o8 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --objects 8
-run o8s1 DSR_STREAMS=1 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --objects 8
-run o8s4 DSR_STREAMS=4 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --objects 8
-run p4096o8 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --objects 8 --pts 4096
-run p4096o64 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-extra --no-cpu-baseline --pts 4096
+run o64 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-extra --no-cpu-baseline --no-config4
+run o8g DSR_GRAPH=1 timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-extra --no-cpu-baseline --no-config4 --objects 8
+run o16 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --objects 16
+run o8 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --objects 8
+run o8s1 DSR_STREAMS=1 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --objects 8
+run o8s4 DSR_STREAMS=4 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --objects 8
+run p4096o8 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --objects 8 --pts 4096
+run p4096o64 timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-extra --no-cpu-baseline --no-config4 --pts 4096
