@@ -237,10 +237,8 @@ struct dsr_batch {
   bool ran = false;
   int runs = 0;
   bool timed = false;               // last run recorded per-kernel events (eager run)
-  // DSR_GRAPH=1: each object group's regular iterations captured as one hipGraph, replayed on
-  // the group's own stream (so the groups stay concurrent), captured on the 2nd dsr_batch_run
-  std::vector<hipGraphExec_t> graphs;
-  long graph_key = -1;              // kernel variants the graphs were captured with
+  hipGraphExec_t graph = nullptr;   // the whole run, captured on the 2nd dsr_batch_run
+  long graph_key = -1;              // kernel variants the graph was captured with
 };
 
 #define DSR_CHECK(ctx, call)                                                        \
@@ -647,8 +645,7 @@ int dsr_batch_destroy(dsr_batch* b) {
   hipSetDevice(ctx->device);
   // the blocks go back to the pool: no kernel of this batch may still be using them
   for (size_t g = 0; g < std::max<size_t>(1, b->groups.size()); ++g) hipStreamSynchronize(ctx->gstream[g]);
-  for (hipGraphExec_t g : b->graphs)
-    if (g) hipGraphExecDestroy(g);
+  if (b->graph) hipGraphExecDestroy(b->graph);
   std::lock_guard<std::mutex> lk(ctx->mu);
   for (auto& e : b->ev)
     if (e) ctx->ev_timing.push_back(e);
@@ -878,43 +875,35 @@ static int jac_variant() {
 }
 
 // dsr_batch_run: with DSR_GRAPH=1 the first run of a batch is enqueued eagerly and from
-// the second on (a re-run batch: streaming keyframes, config 5) each object group's launch
-// sequence — ~6 + 3 x passes launches per iteration — is captured once into a hipGraph on
-// the group's stream; a replay is k_init_state, one graph launch per group stream (fork /
-// join events around them, so the groups run side by side as in an eager run) and
-// k_finalize.  (Round 2 captured the whole fork/join sequence as ONE graph; its replay ran
-// the groups' branches one after another.)  dsr_batch_graph captures up front.  A replayed
-// run records only its total time (kernel events stay out of the graphs: HIP cannot time
-// events recorded inside one), so dsr_batch_stats reports no kernel times.
+// the second on (a re-run batch: streaming keyframes, config 5) the whole multi-stream
+// launch sequence — ~6 + 3 x passes launches per iteration and group — is captured once
+// into a hipGraph and replayed with one launch; dsr_batch_graph captures up front.  A
+// replayed run records only its total time (kernel events stay out of the graph: HIP
+// cannot time events recorded inside one), so dsr_batch_stats reports no kernel times.
 static bool graph_enabled() {        // DSR_GRAPH=1: replay re-run batches as hipGraphs
   const char* ge = getenv("DSR_GRAPH");
   return ge && atoi(ge) != 0;
 }
 static long graph_key() { return ((long)fwd_variant() * 100000 + jac_variant()) * 10 + split_ring(); }
 
-static int enqueue_group_iter(dsr_batch* b, int g, int it, bool timing);
-
 static int batch_capture(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
-  for (hipGraphExec_t e : b->graphs)
-    if (e) hipGraphExecDestroy(e);
-  b->graphs.assign(b->groups.size(), nullptr);
-  for (size_t gi = 0; gi < b->groups.size(); ++gi) {
-    hipStream_t s = ctx->gstream[gi];
-    hipGraph_t g = nullptr;
-    DSR_CHECK(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    int rc = 0;
-    for (int it = 0; it < b->iters && rc == 0; ++it) rc = enqueue_group_iter(b, (int)gi, it, false);
-    const hipError_t ec = hipStreamEndCapture(s, &g);
-    if (rc) {
-      if (g) hipGraphDestroy(g);
-      return rc;
-    }
-    DSR_CHECK(ctx, ec);
-    const hipError_t ei = hipGraphInstantiate(&b->graphs[gi], g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
-    DSR_CHECK(ctx, ei);
+  if (b->graph) {
+    hipGraphExecDestroy(b->graph);
+    b->graph = nullptr;
   }
+  hipGraph_t g = nullptr;
+  DSR_CHECK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  const int rc = batch_enqueue(b, false);      // kernel timing events stay out of the graph
+  const hipError_t ec = hipStreamEndCapture(ctx->stream, &g);
+  if (rc) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  DSR_CHECK(ctx, ec);
+  const hipError_t ei = hipGraphInstantiate(&b->graph, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  DSR_CHECK(ctx, ei);
   b->graph_key = graph_key();
   return 0;
 }
@@ -936,26 +925,13 @@ static int batch_launch(dsr_batch* b) {
     b->timed = true;
     return 0;
   }
-  if (b->graphs.size() != b->groups.size() || b->graph_key != graph_key()) {
+  if (!b->graph || b->graph_key != graph_key()) {
     const int rc = batch_capture(b);
     if (rc) return rc;
   }
-  hipStream_t s0 = ctx->stream;
-  const int G = (int)b->groups.size();
-  DSR_CHECK(ctx, hipEventRecord(b->ev[0], s0));
-  hipLaunchKernelGGL(k_init_state, dim3(b->n_obj), dim3(64), 0, s0, b->n_obj, b->t_in, b->is_oc, b->z_in, b->st,
-                     b->zbuf, b->iters);
-  DSR_CHECK(ctx, hipMemsetAsync(b->diag, 0, sizeof(int) * STD_INTS, s0));
-  DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
-  for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
-  for (int g = 0; g < G; ++g) DSR_CHECK(ctx, hipGraphLaunch(b->graphs[g], ctx->gstream[g]));
-  for (int g = 1; g < G; ++g) {
-    DSR_CHECK(ctx, hipEventRecord(b->join_ev[g], ctx->gstream[g]));
-    DSR_CHECK(ctx, hipStreamWaitEvent(s0, b->join_ev[g], 0));
-  }
-  hipLaunchKernelGGL(k_finalize, dim3((b->n_obj + 63) / 64), dim3(64), 0, s0, b->n_obj, b->st, b->zbuf, b->out);
-  DSR_CHECK(ctx, hipGetLastError());
-  DSR_CHECK(ctx, hipEventRecord(b->ev[1], s0));
+  DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
+  DSR_CHECK(ctx, hipGraphLaunch(b->graph, ctx->stream));
+  DSR_CHECK(ctx, hipEventRecord(b->ev[1], ctx->stream));
   b->spare_run = false;          // a replay runs the regular iterations only (batch_finish)
   b->ran = true;
   b->timed = false;
@@ -1030,15 +1006,14 @@ static int batch_finish(dsr_batch* b) {
   return 0;
 }
 
-// One object group's GN iteration `it` on the group's stream: every launch of optimizer.py's
-// loop body for the group's objects (eager runs interleave the groups' iterations; a graph
-// capture records one group's iterations on its own stream).
-static int enqueue_group_iter(dsr_batch* b, int g, int it, bool timing) {
+static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
   dsr_ctx* ctx = b->ctx;
+  hipStream_t s0 = ctx->stream;
   const int n = b->n_obj;
   const DevDecoder& D = b->dec->D;
   const GNParams P = b->P;
   const int grid = ctx->n_cu;
+  const int cb = (n + 63) / 64;
   const int fv = fwd_variant();
   const FwdKernel fwdk = fwd_kernel(fv);
   const JacKernel jack = jac_kernel();
@@ -1046,95 +1021,85 @@ static int enqueue_group_iter(dsr_batch* b, int g, int it, bool timing) {
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
-  const dsr_batch::Group& gr = b->groups[g];
-  hipStream_t s = ctx->gstream[g];
-  const int ng = gr.n, o0 = gr.o0;
-  const ObjDesc* desc = b->desc + o0;
-  ObjState* st = b->st + o0;
-  float* zbuf = b->zbuf + (size_t)o0 * CODE;
-  float* b0 = b->bias0f + (size_t)o0 * HID;
-  float* b4 = b->bias4f + (size_t)o0 * HID;
-  hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
-  hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
-  ErtArgs ert = b->lite_cfg;
-  ert.dead = b->dead;
-  ert.M = b->M;
-  ert.nth = -P.cut_off;
-  ert.st = b->lite ? st : nullptr;
-  ert.refine = b->refine;
-  ert.diag = b->diag;
-  DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
-                                   (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
-  for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
-    hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                       b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);
-    hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
-                       b->lite ? LTILE : TILE, 0);
-    if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
-    if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
-    if (b->lite)
-      hipLaunchKernelGGL(litek, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
-                         b->cand, b0, b4, b->dense, ert);
-    else
-      hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                         b0, b4, b->dense, gr.sync, ert, MaskArgs{nullptr, nullptr, nullptr, nullptr});
-    if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
-  }
-  if (b->lite) {                             // exact split-fp16 decode of the band samples
-    hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->M,
-                       b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt,
-                       b->ma.slotmap);
-    hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                       b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
-    hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
-                       (b->ma.pts && fv == 12) ? 1 : 0);
-    if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
-    const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
-    if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
-      hipLaunchKernelGGL(fwd16_kernel<512>(), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
-                         b->cand, b0, b4, b->dense, gr.sync, ex, b->ma);
-    else
-      hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
-                         b0, b4, b->dense, gr.sync, ex, MaskArgs{nullptr, nullptr, nullptr, nullptr});
-    if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
-  }
-  const bool keep = b->lite && b->ma.msk && fv == 12;
-  const int je = 2 * (np + (b->lite ? 1 : 0));
-  hipLaunchKernelGGL(k_render_rays, dim3(gr.n_rch), dim3(RENDER_RAYS), render_lds_bytes(b->M), s,
-                     gr.rchunks, desc, st, b->rays, b->dobs, P, b->dense, b->kst, b->rst,
-                     keep ? b->sst : nullptr, (const int*)b->ma.slotmap, gr.ccnt);
-  hipLaunchKernelGGL(k_render_gather, dim3(gr.n_rch), dim3(256), 0, s, gr.rchunks, desc, st, gr.ccnt, b->M,
-                     b->kst, b->rst, b->sst, b->kpts, b->kres, keep ? b->kslot : nullptr);
-  hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
-  if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
-  hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
-                     b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
-                     (const float4*)nullptr, (float*)nullptr, (float*)nullptr,
-                     keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
-  if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
-  float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
-  hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred, it,
-                     b->counts + (size_t)o0 * NCOUNT, n);
-  hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, sred,
-                     b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
-                     b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
-                     b->tr_i ? b->tr_i + (size_t)o0 * 2 : nullptr, n);
-  return 0;
-}
-
-static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
-  dsr_ctx* ctx = b->ctx;
-  hipStream_t s0 = ctx->stream;
-  const int n = b->n_obj;
-  const int cb = (n + 63) / 64;
-  const int G = (int)b->groups.size();
   DSR_CHECK(ctx, hipEventRecord(b->fork_ev, s0));
   for (int g = 1; g < G; ++g) DSR_CHECK(ctx, hipStreamWaitEvent(ctx->gstream[g], b->fork_ev, 0));
-  for (int it = it0; it < it1; ++it)
+  for (int it = it0; it < it1; ++it) {
     for (int g = 0; g < G; ++g) {             // groups interleaved, one stream each
-      const int rc = enqueue_group_iter(b, g, it, timing);
-      if (rc) return rc;
+      const dsr_batch::Group& gr = b->groups[g];
+      hipStream_t s = ctx->gstream[g];
+      const int ng = gr.n, o0 = gr.o0;
+      const ObjDesc* desc = b->desc + o0;
+      ObjState* st = b->st + o0;
+      float* zbuf = b->zbuf + (size_t)o0 * CODE;
+      float* b0 = b->bias0f + (size_t)o0 * HID;
+      float* b4 = b->bias4f + (size_t)o0 * HID;
+      hipEvent_t* ev = b->ev.data() + 2 + ((size_t)it * G + g) * epi;
+      hipLaunchKernelGGL(k_iter_begin, dim3(ng), dim3(512), 0, s, ng, desc, st, zbuf, D, P, b0, b4, b->dobs);
+      ErtArgs ert = b->lite_cfg;
+      ert.dead = b->dead;
+      ert.M = b->M;
+      ert.nth = -P.cut_off;
+      ert.st = b->lite ? st : nullptr;
+      ert.refine = b->refine;
+      ert.diag = b->diag;
+      DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
+                                       (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
+      for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
+        hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
+                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
+                           b->lite ? LTILE : TILE, 0);
+        if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
+        if (b->lite)
+          hipLaunchKernelGGL(litek, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+                             b->cand, b0, b4, b->dense, ert);
+        else
+          hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                             b0, b4, b->dense, gr.sync, ert, MaskArgs{nullptr, nullptr, nullptr, nullptr});
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz + 1], s));
+      }
+      if (b->lite) {                             // exact split-fp16 decode of the band samples
+        hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->M,
+                           b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt,
+                           b->ma.slotmap);
+        hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                           b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
+        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
+                           (b->ma.pts && fv == 12) ? 1 : 0);
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
+        const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
+        if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
+          hipLaunchKernelGGL(fwd16_kernel<512>(), dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc,
+                             b->cand, b0, b4, b->dense, gr.sync, ex, b->ma);
+        else
+          hipLaunchKernelGGL(fwdk, dim3(grid), dim3(512), 0, s, D, gr.tiles_f, gr.nt_f, desc, b->cand,
+                             b0, b4, b->dense, gr.sync, ex, MaskArgs{nullptr, nullptr, nullptr, nullptr});
+        if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np + 1], s));
+      }
+      const bool keep = b->lite && b->ma.msk && fv == 12;
+      const int je = 2 * (np + (b->lite ? 1 : 0));
+      hipLaunchKernelGGL(k_render_rays, dim3(gr.n_rch), dim3(RENDER_RAYS), render_lds_bytes(b->M), s,
+                         gr.rchunks, desc, st, b->rays, b->dobs, P, b->dense, b->kst, b->rst,
+                         keep ? b->sst : nullptr, (const int*)b->ma.slotmap, gr.ccnt);
+      hipLaunchKernelGGL(k_render_gather, dim3(gr.n_rch), dim3(256), 0, s, gr.rchunks, desc, st, gr.ccnt, b->M,
+                         b->kst, b->rst, b->sst, b->kpts, b->kres, keep ? b->kslot : nullptr);
+      hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
+      hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
+                         b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
+                         (const float4*)nullptr, (float*)nullptr, (float*)nullptr,
+                         keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
+      if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
+      float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
+      hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred, it,
+                         b->counts + (size_t)o0 * NCOUNT, n);
+      hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, sred,
+                         b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
+                         b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
+                         b->tr_i ? b->tr_i + (size_t)o0 * 2 : nullptr, n);
     }
+  }
   for (int g = 1; g < G; ++g) {
     DSR_CHECK(ctx, hipEventRecord(b->join_ev[g], ctx->gstream[g]));
     DSR_CHECK(ctx, hipStreamWaitEvent(s0, b->join_ev[g], 0));
