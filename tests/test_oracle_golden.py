@@ -217,3 +217,37 @@ def test_kitti_margin_fixtures_run_the_rotation_prior():
             r = tco[:3, :3] / np.cbrt(np.linalg.det(tco[:3, :3]))
             assert 1.0 + r[1, 1] > 1e-6, (p, e)
         assert (f["margin_rot_ulps"][:n_it] >= 4.0).all()
+
+
+def _edge_case_inputs(f, c):
+    """Golden F10 (tests/golden/make_edge.py): case ``c``'s (pts, rays, depth)."""
+    n, nr, nf = int(f[c + "_n_pts"]), int(f[c + "_n_rays"]), int(f[c + "_n_fg"])
+    n_fg_all = f["obj_depth"].shape[0]
+    rays = f["obj_rays"][n_fg_all:] if c == "no_fg_rays" else f["obj_rays"][:nr]
+    assert rays.shape[0] == nr
+    return f["obj_pts"][:n], rays, f["obj_depth"][:nf]
+
+
+def test_oracle_edge_cases_f10(oracle_dec):
+    """Empty and ragged inputs (F10): no surface points / no rays fail like the reference
+    (is_good False, loss 0. — optimizer.py:132-145), one point, background-only and
+    foreground-only rays give the reference's trajectory (K each iteration, final loss);
+    pose-only GN and the zhjd query on no points give NaN (optimizer.py:62-87, 207-213)."""
+    f = golden("f10_edge.npz")
+    P = O.OptimParams.from_cfg(dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
+                                                                        num_iterations=int(f["num_iterations"]))))
+    for c in f["cases"]:
+        c = str(c)
+        pts, rays, depth = _edge_case_inputs(f, c)
+        r = O.reconstruct_object(oracle_dec, P, f["obj_t_cam_obj"], pts, rays, depth)
+        assert r.is_good == bool(f[c + "_is_good"]), c
+        if not r.is_good:
+            assert r.loss == 0.0 == float(f[c + "_loss"]) and r.t_cam_obj is None, c
+            continue
+        assert [t.k for t in r.trace] == f[c + "_it_k"].tolist(), c
+        assert abs(r.loss - float(f[c + "_loss"])) <= 1e-4 * abs(float(f[c + "_loss"])), c
+    Pk = O.OptimParams.from_cfg(S.KITTI_OPTIM)
+    z = np.zeros(64, np.float32)
+    T = O.estimate_pose_cam_obj(oracle_dec, Pk, f["pose_t_se3"], float(f["pose_scale"]), f["obj_pts"][:0], z)
+    assert np.isnan(T).all() and np.isnan(f["pose_empty_out"]).all()
+    assert np.isnan(O.compute_sdf_loss_objectpoint(oracle_dec, f["obj_pts"][:0], z)) and np.isnan(f["zhjd_empty_out"])
