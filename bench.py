@@ -505,6 +505,21 @@ def main():
         del os.environ["DSR_LITE"]
         out["value_exact"] = n_job * k / dt
         out["value_exact_note"] = "DSR_LITE=0: no classification pass, every in-ball sample decoded exactly"
+        # the three MFMA kernels with the job on ONE stream: per-launch rates without the other
+        # object group's concurrent kernels inside each launch's duration; the
+        # headline roofline above is the timed region's, with both groups overlapping
+        os.environ["DSR_STREAMS"] = "1"
+        one = ResidentShard(opt, objs)
+        one.run()
+        one.run()
+        st1 = L.Stats()
+        ctx.check(lib.dsr_batch_stats(one.handle, C.byref(st1)), "stats")
+        one.close()
+        del os.environ["DSR_STREAMS"]
+        r1 = kernel_rooflines(stats_sum({}, st1))
+        out["rooflines_one_stream"] = {name: {k2: e[k2] for k2 in ("achieved_tflops", "peak_tflops", "frac_of_peak",
+                                                                   "avg_launch_ms", "launches")}
+                                       for name, e in r1.items()}
         out["keyframe"] = keyframe_leg(dec)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
