@@ -101,3 +101,15 @@ def test_missing_library_fails_loudly(tmp_path):
 
     with pytest.raises(L.DsrError):
         L.load_library(str(tmp_path / "nope.so"))
+
+
+def test_c_caller_links_and_fails_loudly_without_a_device():
+    """examples/dsr_c_smoke.c — the ABI from C, no Python: it links
+    against libdsr.so, its DSR_ABI_VERSION matches the library's, and without a HIP device
+    context creation reports -3 (no CPU fallback)."""
+    exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", "dsr_c_smoke")
+    assert os.path.isfile(exe), "built by make -C dsp-slam-rgbd_amd/csrc"
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    rc = int(p.stdout.split()[-1])
+    assert rc in (0, -3)

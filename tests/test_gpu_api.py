@@ -258,3 +258,37 @@ def test_empty_and_ragged_inputs_vs_reference_f10(gpu_decoder):
                                            (f["pose_t_se3"], float(f["pose_scale"]), f["obj_pts"], z)])
     assert np.isnan(Tb[0]).all() and np.isfinite(Tb[1]).all()
     assert np.isnan(kopt.compute_sdf_loss_objectpoint_zhjd(f["obj_pts"][:0], z))
+
+
+def test_c_caller_reconstructs_like_the_python_api(gpu_decoder, tmp_path):
+    """The C ABI driven from C (examples/dsr_c_smoke.c: dsr_ctx_create, dsr_decoder_load with
+    the folded weights, dsr_reconstruct_batch) gives the records the Python API gets for the
+    same objects, bitwise — the library, not the binding, is the product."""
+    import os
+    import subprocess
+
+    from conftest import REPO
+
+    objs = [S.redwood_object(i, n_pts=256 + 64 * i) for i in range(3)]
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=3)
+    ref = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
+    gpu_decoder._flat.tofile(str(tmp_path / "weights.f32"))
+    p = opt.params
+    np.array([p.k1, p.k2, p.k3, p.k4, p.b1, p.b2, p.lr, p.s_damp, p.num_iterations, p.code_len,
+              p.num_depth_samples, p.cut_off, p.pose_only_iterations], np.float32).tofile(str(tmp_path / "params.f32"))
+    with open(tmp_path / "objects.bin", "wb") as fh:
+        fh.write(np.int32(len(objs)).tobytes())
+        for o in objs:
+            fh.write(np.array([o.pts.shape[0], o.rays.shape[0], o.depth.shape[0]], np.int32).tobytes())
+            for a in (o.t_cam_obj, o.pts, o.rays, o.depth):
+                fh.write(np.ascontiguousarray(a, np.float32).tobytes())
+    exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", "dsr_c_smoke")
+    run = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert run.returncode == 0, run.stdout + run.stderr
+    from reconstruct import _libdsr as L
+
+    outs = (L.ObjectOut * len(objs)).from_buffer_copy((tmp_path / "out.bin").read_bytes())
+    for o, r in zip(outs, ref):
+        assert bool(o.is_good) == r["is_good"] and np.float32(o.loss) == np.float32(r["loss"])
+        assert np.array_equal(np.ctypeslib.as_array(o.t_cam_obj).reshape(4, 4), r["t_cam_obj"])
+        assert np.array_equal(np.ctypeslib.as_array(o.code), r["code"])
