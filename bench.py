@@ -386,6 +386,7 @@ def main():
 
     for _ in range(args.warmup):
         shard.run()
+
     barrier()
     acc = {}
     n_good = 0
@@ -475,6 +476,9 @@ def main():
             "lite_broken_blocks": acc.get("lite_broken_blocks"),
             "test_hooks": acc.get("test_hooks"),
             "ranks": ranks,
+            # device wall of one run (HIP events around dsr_batch_run's work, rank 0): the rest of
+            # ms_per_step is host time (launch, download, packing, stats)
+            "device_ms_per_step": round(acc["total_ms"] / args.steps, 3) if acc else None,
             "good_fraction": n_good / float(n_job * args.steps),
             # inputs handed over in host memory: the upload added to one step
             "host_inclusive_value": n_job / (elapsed / args.steps + create_s),

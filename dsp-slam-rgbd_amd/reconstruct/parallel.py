@@ -125,26 +125,31 @@ class ResidentShard:
             ctx = self.opt._ctx
             ctx.check(ctx.lib.dsr_batch_run(self.handle), "dsr_batch_run")
 
-    def records(self):
-        """Wait for the shard, download it and pack its records (this rank's block)."""
-        rec = np.zeros((self.width, REC), np.float32)
-        rec[:, 83] = -1.0
+    def download(self):
+        """Wait for the shard's run and copy its per-object results to host memory."""
         if self.handle is not None:
             ctx = self.opt._ctx
             ctx.check(ctx.lib.dsr_batch_download(self.handle, self.outs), "dsr_batch_download")
+
+    def pack_records(self):
+        """This rank's block of records from the last ``download()`` (host work only: the
+        device buffers are free for the next ``launch()`` once ``download()`` returned)."""
+        rec = np.zeros((self.width, REC), np.float32)
+        rec[:, 83] = -1.0
+        if self.handle is not None:
             res = [self.opt._result(self.outs[k]) for k in range(len(self.mine))]
             for k, r in enumerate(res):
                 r["iters_done"] = int(self.outs[k].iters_done)
             rec[:len(self.mine)] = pack(res, self.mine)
         return rec
 
-    def run(self):
-        """One step: launch, wait, gather. Results in input order on rank 0, None elsewhere.
-        ``last_gather_s`` holds the host time of this step's gather (the RCCL collective)."""
+    def finish(self):
+        """Pack the downloaded shard and gather every rank's records: results in input
+        order on rank 0, None elsewhere. ``last_gather_s`` holds the host time of the
+        gather (the RCCL collective)."""
         import time
 
-        self.launch()
-        rec = self.records()
+        rec = self.pack_records()
         if not self.dist:
             self.last_gather_s = 0.0
             return unpack_all(rec, self.n)
@@ -152,6 +157,12 @@ class ResidentShard:
         allrec = gather_records(rec, self.width, self.group, self.device)
         self.last_gather_s = time.perf_counter() - t0
         return None if allrec is None else unpack_all(allrec, self.n)
+
+    def run(self):
+        """One step: launch, wait, gather. Results in input order on rank 0, None elsewhere."""
+        self.launch()
+        self.download()
+        return self.finish()
 
     def close(self):
         if self.handle is not None:

@@ -158,13 +158,20 @@ def _resident_worker(rank, world, port, q):
         shard = ResidentShard(_fake_optimizer(), _objects())
         first = shard.run()
         second = shard.run()                 # inputs stay resident: a re-run gives the same records
+        shard.launch()                       # bench.py's overlapped steps: step s+1 launched
+        shard.download()                     # before step s's records are packed and gathered
+        shard.launch()
+        third = shard.finish()
+        shard.download()
+        fourth = shard.finish()
         if rank == 0:
             q.put({"mine": shard.mine, "shards": shard.shards, "gather": shard.last_gather_s,
                    "res": [(r["is_good"], r["loss"], None if r["t_cam_obj"] is None else r["t_cam_obj"].tolist(),
                             r["iters_done"]) for r in first],
-                   "same": all(a["loss"] == b["loss"] for a, b in zip(first, second))})
+                   "same": all(a["loss"] == b["loss"] == c["loss"] == d["loss"]
+                               for a, b, c, d in zip(first, second, third, fourth))})
         else:
-            assert first is None and second is None
+            assert first is None and second is None and third is None and fourth is None
         shard.close()
     finally:
         dist.destroy_process_group()
