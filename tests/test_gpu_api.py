@@ -292,3 +292,32 @@ def test_c_caller_reconstructs_like_the_python_api(gpu_decoder, tmp_path):
         assert bool(o.is_good) == r["is_good"] and np.float32(o.loss) == np.float32(r["loss"])
         assert np.array_equal(np.ctypeslib.as_array(o.t_cam_obj).reshape(4, 4), r["t_cam_obj"])
         assert np.array_equal(np.ctypeslib.as_array(o.code), r["code"])
+
+
+def test_replicated_object_matches_the_original(gpu_decoder):
+    """Large inputs through a size-independent property: every term of the reference's
+    objective is a mean (loss.py:22-43 over surface points, :60-166 over valid samples and
+    render points), so an object whose surface points are repeated 16x and whose foreground
+    and background rays are each repeated 8x (17,984 rays x 50 samples, 32,768 points) has
+    the same Gauss-Newton trajectory as the original up to summation order.  Exercises the
+    tile tables, ray chunks and slot reductions at 16x / 8x the metric object's sizes.
+    One iteration: pose and loss within 1e-6, code within 1e-4 (measured 1e-9 / 0 / 2.6e-6).  Ten iterations: pose and loss within
+    1e-3; the code within 0.1 of its largest entry, because the code directions the data
+    barely constrain amplify rounding over the trajectory — the reference's own 64 ulp-
+    perturbed starts (tests/golden/f4_traj_kitti0/5.npz: ens64_code) end with codes whose
+    largest deviation from the unperturbed run is, at the median member, 0.10 / 0.35 of the
+    code's largest entry."""
+    ob = S.kitti_object(3, base_seed=1000)
+    n_fg = ob.depth.shape[0]
+    big_rays = np.concatenate([np.tile(ob.rays[:n_fg], (8, 1)), np.tile(ob.rays[n_fg:], (8, 1))])
+    for iters, tol_t, tol_z in ((1, 1e-6, 1e-4), (10, 1e-3, 1e-1)):
+        opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=iters)
+        base = opt.reconstruct_object(ob.t_cam_obj, ob.pts, ob.rays, ob.depth)
+        big = opt.reconstruct_object(ob.t_cam_obj, np.tile(ob.pts, (16, 1)), big_rays, np.tile(ob.depth, 8))
+        assert base["is_good"] and big["is_good"]
+        assert base["iters_done"] == big["iters_done"] == iters
+        d_t = np.abs(big["t_cam_obj"] - base["t_cam_obj"]).max() / np.abs(base["t_cam_obj"]).max()
+        d_z = np.abs(big["code"] - base["code"]).max() / max(1e-6, np.abs(base["code"]).max())
+        d_l = abs(big["loss"] - base["loss"]) / abs(base["loss"])
+        print(f"{iters} iterations, replicated vs original: pose {d_t:.2e} code {d_z:.2e} loss {d_l:.2e}")
+        assert d_t <= tol_t and d_z <= tol_z and d_l <= tol_t
