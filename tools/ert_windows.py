@@ -4,7 +4,7 @@ Offline analysis on the oracle (numpy fp32) along a recorded reference trajector
 per ray, the in-ball run and the rank of the first sample with sdf <= -th; decoded
 samples under (a) the fixed rank windows of k_sample_pass, (b) the minimum (every
 sample up to the first full one), (c) windows seeded per ray from the previous
-iteration's termination rank.
+iteration's termination rank (the fixed windows on the first iteration).
 
 Usage: python tools/ert_windows.py [f4 fixture name] [windows...]
 """
@@ -58,10 +58,11 @@ for e in range(int(f["n_iters_run"])):
             fixed[r] += min(b, cnt[r]) - a
             if term[r] >= 0 and term[r] < b:
                 break
-    # predicted: first window [0, p) with p = previous termination + 2 (or the run), then +4 windows
-    pred = np.zeros(R, int)
-    for r in range(R):
-        p = cnt[r] if prev is None or prev[r] < 0 else min(cnt[r], prev[r] + 3)
+    # predicted: the fixed windows on the first iteration; then a first window [0, p) with
+    # p = previous termination + 1 (or the run), then +4 windows
+    pred = fixed.copy() if prev is None else np.zeros(R, int)
+    for r in range(R if prev is not None else 0):
+        p = cnt[r] if prev[r] < 0 else min(cnt[r], prev[r] + 1)
         bnds = [0, p] + list(range(p + 4, cnt[r] + 4, 4))
         for a, b in zip(bnds[:-1], bnds[1:]):
             if a >= cnt[r]:
