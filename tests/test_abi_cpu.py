@@ -113,3 +113,16 @@ def test_c_caller_links_and_fails_loudly_without_a_device():
     assert p.returncode == 0, p.stderr
     rc = int(p.stdout.split()[-1])
     assert rc in (0, -3)
+
+
+@pytest.mark.parametrize("exe_name", ["dsr_c_stress", "dsr_c_stress_asan"])
+def test_c_stress_no_device_paths(exe_name):
+    """examples/dsr_c_stress.c without inputs: the argument checks and error reporting of
+    the entry points that validate before touching the device, against the shipped library
+    and against libdsr_asan.so (host code under AddressSanitizer + UBSan, leak checking
+    on).  The device paths of the same driver run in test_gpu_api.py."""
+    exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", exe_name)
+    assert os.path.isfile(exe), "built by make -C dsp-slam-rgbd_amd/csrc"
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "stress ok" in p.stdout

@@ -260,6 +260,20 @@ def test_empty_and_ragged_inputs_vs_reference_f10(gpu_decoder):
     assert np.isnan(kopt.compute_sdf_loss_objectpoint_zhjd(f["obj_pts"][:0], z))
 
 
+def _write_c_inputs(d, dec, opt, objs):
+    """The input files of examples/dsr_c_smoke.c / dsr_c_stress.c (their headers)."""
+    dec._flat.tofile(str(d / "weights.f32"))
+    p = opt.params
+    np.array([p.k1, p.k2, p.k3, p.k4, p.b1, p.b2, p.lr, p.s_damp, p.num_iterations, p.code_len,
+              p.num_depth_samples, p.cut_off, p.pose_only_iterations], np.float32).tofile(str(d / "params.f32"))
+    with open(d / "objects.bin", "wb") as fh:
+        fh.write(np.int32(len(objs)).tobytes())
+        for o in objs:
+            fh.write(np.array([o.pts.shape[0], o.rays.shape[0], o.depth.shape[0]], np.int32).tobytes())
+            for a in (o.t_cam_obj, o.pts, o.rays, o.depth):
+                fh.write(np.ascontiguousarray(a, np.float32).tobytes())
+
+
 def test_c_caller_reconstructs_like_the_python_api(gpu_decoder, tmp_path):
     """The C ABI driven from C (examples/dsr_c_smoke.c: dsr_ctx_create, dsr_decoder_load with
     the folded weights, dsr_reconstruct_batch) gives the records the Python API gets for the
@@ -272,16 +286,7 @@ def test_c_caller_reconstructs_like_the_python_api(gpu_decoder, tmp_path):
     objs = [S.redwood_object(i, n_pts=256 + 64 * i) for i in range(3)]
     opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=3)
     ref = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
-    gpu_decoder._flat.tofile(str(tmp_path / "weights.f32"))
-    p = opt.params
-    np.array([p.k1, p.k2, p.k3, p.k4, p.b1, p.b2, p.lr, p.s_damp, p.num_iterations, p.code_len,
-              p.num_depth_samples, p.cut_off, p.pose_only_iterations], np.float32).tofile(str(tmp_path / "params.f32"))
-    with open(tmp_path / "objects.bin", "wb") as fh:
-        fh.write(np.int32(len(objs)).tobytes())
-        for o in objs:
-            fh.write(np.array([o.pts.shape[0], o.rays.shape[0], o.depth.shape[0]], np.int32).tobytes())
-            for a in (o.t_cam_obj, o.pts, o.rays, o.depth):
-                fh.write(np.ascontiguousarray(a, np.float32).tobytes())
+    _write_c_inputs(tmp_path, gpu_decoder, opt, objs)
     exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", "dsr_c_smoke")
     run = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stdout + run.stderr
@@ -292,6 +297,67 @@ def test_c_caller_reconstructs_like_the_python_api(gpu_decoder, tmp_path):
         assert bool(o.is_good) == r["is_good"] and np.float32(o.loss) == np.float32(r["loss"])
         assert np.array_equal(np.ctypeslib.as_array(o.t_cam_obj).reshape(4, 4), r["t_cam_obj"])
         assert np.array_equal(np.ctypeslib.as_array(o.code), r["code"])
+
+
+def _stress(exe_name, d, **env):
+    import os
+    import subprocess
+
+    from conftest import REPO
+
+    exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", exe_name)
+    return subprocess.run([exe, str(d)], capture_output=True, text=True, timeout=300,
+                          env=dict(os.environ, UBSAN_OPTIONS="print_stacktrace=1", **env))
+
+
+@pytest.mark.parametrize("exe_name", ["dsr_c_stress", "dsr_c_stress_asan"])
+def test_c_stress_every_entry_point(gpu_decoder, tmp_path, exe_name):
+    """examples/dsr_c_stress.c on the device: every C entry point with cross-checks — one-shot
+    batch twice and with a trace (bitwise), resident batches run / queried / downloaded three
+    times and re-created from the pool, graph capture + four replays, two contexts through
+    dsr_reconstruct_multi, sdf_eval with and without the Jacobian, pose-only single vs batched
+    with an empty object, the mesher at ample and too small capacities, forced audit
+    violations redone in the spare iteration, error paths of a live context — bitwise equal where the ABI promises it (72k checks).  ``dsr_c_stress_asan``
+    runs the same checks with the library's HOST code under AddressSanitizer + UBSan
+    (libdsr_asan.so; there is no GPU sanitizer on this pool): any heap overflow, use after
+    free or undefined behaviour in the batch / pool / event / graph / thread bookkeeping
+    aborts it."""
+    objs = [S.kitti_object(i, base_seed=1000, n_pts=512) for i in range(5)]
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=3)
+    _write_c_inputs(tmp_path, gpu_decoder, opt, objs)
+    # quick exit: past its last check the driver skips the HIP runtime's static destructors,
+    # where host ASan's device-allocator hook trips over the runtime's own teardown (r3k)
+    run = _stress(exe_name, tmp_path, ASAN_OPTIONS="detect_leaks=0", DSR_STRESS_QUICK_EXIT="1")
+    assert run.returncode == 0, (run.stdout + run.stderr)[-6000:]
+    assert "stress ok" in run.stdout, run.stdout
+
+
+def test_c_stress_leaks_nothing_beyond_the_runtime(gpu_decoder, tmp_path):
+    """Differential leak check (LeakSanitizer, host-ASan build): the HIP runtime keeps ~116
+    allocations from context creation on, made through libstdc++'s operator new, whose frames
+    the sanitizer cannot attribute.  So the run with every section of the stress driver
+    (resident batches, pool re-use, traces, reconstruct_multi's threads, queries, mesher, pose
+    batches, error paths) must leave exactly the allocations the run with none of them
+    leaves: a batch, event, pool block or thread record of libdsr that is never freed would
+    add to them.  Graph capture is left out of both: HIP's graph implementation keeps ~43 MB
+    and 9 unattributed allocations after hipGraphExecDestroy / hipGraphDestroy
+    (tools/leak_probe.sh, r3k) while libdsr destroys both (dsr_api.hip: batch_capture,
+    dsr_batch_destroy)."""
+    import re
+
+    objs = [S.kitti_object(i, base_seed=1000, n_pts=512) for i in range(5)]
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=3)
+    _write_c_inputs(tmp_path, gpu_decoder, opt, objs)
+
+    def leaked(skip):
+        r = _stress("dsr_c_stress_asan", tmp_path, ASAN_OPTIONS="detect_leaks=1", DSR_STRESS_SKIP=skip)
+        assert "stress ok" in r.stdout, (r.stdout + r.stderr)[-4000:]
+        m = re.search(r"SUMMARY: AddressSanitizer: (\d+) byte\(s\) leaked in (\d+) allocation", r.stderr)
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+    every = leaked("graph")
+    none = leaked("graph,trace,resident,redo,multi,query,mesher,errors")
+    assert every == none, (every, none)
 
 
 def test_replicated_object_matches_the_original(gpu_decoder):
