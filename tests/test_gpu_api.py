@@ -260,6 +260,45 @@ def test_empty_and_ragged_inputs_vs_reference_f10(gpu_decoder):
     assert np.isnan(kopt.compute_sdf_loss_objectpoint_zhjd(f["obj_pts"][:0], z))
 
 
+def _device_free_bytes():
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    return free.value
+
+
+def test_keyframe_stream_reaches_a_memory_steady_state(gpu_decoder):
+    """A keyframe stream (config 5: LocalMapping runs one batch per keyframe for as long as
+    the sequence lasts) cycling through three keyframe shapes — 2, 3 and 4 detections of
+    different point and ray counts, so the pooled device blocks come in several sizes —
+    holds a constant device footprint once each shape has run: 36 keyframes after the
+    first cycle leave the device's free memory unchanged (a batch block or a pooled block
+    that is never reused or freed would take from it), and the repeated keyframes give the
+    same results bitwise."""
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood", iters=2)
+    shapes = []
+    for k, n_det in enumerate((2, 3, 4)):
+        obs = [S.redwood_object(60 + 5 * k + i, n_pts=256 + 128 * ((i + k) % 3)) for i in range(n_det)]
+        shapes.append([(o.t_cam_obj, o.pts, o.rays, o.depth, None, False) for o in obs])
+    first = [opt.reconstruct_keyframe(d) for d in shapes]
+    for d in shapes:
+        opt.reconstruct_keyframe(d)
+    free0 = _device_free_bytes()
+    for rep in range(12):
+        for k, d in enumerate(shapes):
+            h = opt.reconstruct_keyframe_async(d)
+            res = h.wait()
+            if rep == 11:
+                for a, b in zip(first[k], res):
+                    assert a["is_good"] == b["is_good"] and a["loss"] == b["loss"]
+                    if a["is_good"]:
+                        assert np.array_equal(a["code"], b["code"])
+    free1 = _device_free_bytes()
+    assert free1 == free0, (free0, free1, free0 - free1)
+
+
 def _write_c_inputs(d, dec, opt, objs):
     """The input files of examples/dsr_c_smoke.c / dsr_c_stress.c (their headers)."""
     dec._flat.tofile(str(d / "weights.f32"))
