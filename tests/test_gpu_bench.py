@@ -37,14 +37,16 @@ def _bench(n, dump, extra=(), env_extra=None, launcher=()):
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.timeout(300)
-def test_bench_two_ranks_gather_equals_one_process(tmp_path):
-    two = _bench(2, str(tmp_path / "two.npy"))
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_two_ranks_gather_equals_one_process(tmp_path, n):
+    """n gloo ranks on device 0 (4: the 2-objects-per-rank shards of an 8-object job)."""
+    two = _bench(n, str(tmp_path / "two.npy"))
     one = _bench(1, str(tmp_path / "one.npy"))
-    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["n_gpus"] == n and one["n_gpus"] == 1
     r = two["ranks"]
-    assert r["world_size_observed"] == 2 and r["backend"] == "gloo" and len(r["rank_seconds"]) == 2
-    assert sorted(r["shard_objects"]) == [4, 4] and r["gather_ms_per_step"] > 0
+    assert r["world_size_observed"] == n and r["backend"] == "gloo" and len(r["rank_seconds"]) == n
+    assert sorted(r["shard_objects"]) == [8 // n] * n and r["gather_ms_per_step"] > 0
     assert two["config"]["objects"] == one["config"]["objects"] == 8
     a, b = np.load(tmp_path / "two.npy"), np.load(tmp_path / "one.npy")
     assert a.shape == b.shape == (8, 83)
