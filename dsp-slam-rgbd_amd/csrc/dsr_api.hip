@@ -665,6 +665,8 @@ int dsr_batch_destroy(dsr_batch* b) {
   return 0;
 }
 
+static bool graph_enabled();
+
 static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
                              int n_obj, const dsr_object_in* in, bool trace, dsr_batch** out) {
   if (!ctx || !dec || !p || !out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
@@ -723,8 +725,13 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     // large objects (a strong-scaled shard of 8-16 KITTI objects is bound by its latency
     // kernels, which the extra groups hide: 8 objects 317 -> 333 obj/s), 2 again for small
     // batches of small objects (8 Redwood keyframe hypotheses: 5.31 -> 5.16 ms)
+    // Under DSR_GRAPH=1 the default is ONE group: ROCm 7.2 replays a captured multi-stream
+    // fork/join as a graph 1.6x slower than the eager groups (keyframe batch 8.4 vs 5.2 ms,
+    // whatever DEBUG_HIP_FORCE_GRAPH_QUEUES / DEBUG_CLR_GRAPH_PACKET_CAPTURE say), while a
+    // one-group graph replays 3% faster than a one-group eager run (5.31 vs 5.46 ms; r3k,
+    // tools/graph_queues.py).  Results are bitwise the same for any grouping.
     const char* e = getenv("DSR_STREAMS");
-    int G = e ? atoi(e) : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
+    int G = e ? atoi(e) : graph_enabled() ? 1 : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
     G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
     if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
     for (int g = 0; g < G; ++g) {
