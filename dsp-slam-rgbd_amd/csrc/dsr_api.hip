@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -698,6 +699,13 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     if (x.n_depth < 0 || x.n_depth > x.n_rays || (x.n_depth > 0 && !x.depth)) {
       dsr_batch_destroy(b);
       return fail(ctx, "depth must hold at most n_rays foreground values");
+    }
+    // device offsets and tile tables are 32-bit: a batch holds at most 2^31 - 1 ray samples
+    // plus surface points (HBM runs out first with kept masks, ~580 B per sample; without
+    // them ~70 B per sample would let a batch pass the limit) — split larger jobs
+    if ((long long)x.n_rays * M + cand_off + x.n_pts + pts_off > (long long)INT_MAX) {
+      dsr_batch_destroy(b);
+      return fail(ctx, "batch too large: more than 2^31 - 1 ray samples + surface points (split it)");
     }
     ObjDesc d{};
     d.pts_off = pts_off; d.n_pts = x.n_pts;

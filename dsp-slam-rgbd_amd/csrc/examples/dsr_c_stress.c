@@ -112,6 +112,13 @@ static void live_error_paths(dsr_ctx* ctx, const dsr_decoder* dec, const float* 
   CHECK(dsr_reconstruct_batch(ctx, dec, p, 1, NULL, out, NULL) < 0, "NULL in accepted");
   dsr_batch* b = NULL;
   CHECK(dsr_batch_create(ctx, dec, p, 0, in, &b) < 0 && b == NULL, "empty batch accepted");
+  /* more ray samples than 32-bit device offsets hold: refused before any input is read (the
+     ray pointer below covers only the real object's rays) */
+  dsr_object_in big = in[0];
+  big.n_rays = 50000000;
+  big.n_depth = 0;
+  CHECK(dsr_batch_create(ctx, dec, p, 1, &big, &b) < 0 && b == NULL, "2.5e9-sample batch accepted");
+  CHECK(strstr(dsr_last_error(ctx), "too large") != NULL, "%s", dsr_last_error(ctx));
   CHECK(dsr_sdf_eval(ctx, dec, NULL, NULL, 4, NULL, NULL) < 0, "sdf_eval NULLs accepted");
   dsr_mesher* m = NULL;
   CHECK(dsr_mesher_create(ctx, dec, NULL, 8, &m) < 0 && m == NULL, "mesher without grid accepted");
