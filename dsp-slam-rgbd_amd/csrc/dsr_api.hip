@@ -949,6 +949,10 @@ static int batch_launch(dsr_batch* b) {
     if (rc) return rc;
   }
   DSR_CHECK(ctx, hipEventRecord(b->ev[0], ctx->stream));
+  // poison the out-records first: a replay's k_finalize (inside the graph) rewrites every one,
+  // so a download that ever saw these bytes would expose work ordered wrongly around the graph
+  // launch (test_graph_replays_never_return_stale_records) instead of returning stale results
+  DSR_CHECK(ctx, hipMemsetAsync(b->out, 0xff, sizeof(dsr_object_out) * b->n_obj, ctx->stream));
   DSR_CHECK(ctx, hipGraphLaunch(b->graph, ctx->stream));
   DSR_CHECK(ctx, hipEventRecord(b->ev[1], ctx->stream));
   b->spare_run = false;          // a replay runs the regular iterations only (batch_finish)

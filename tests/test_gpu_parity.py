@@ -521,6 +521,39 @@ def test_graph_replay_bitwise(gpu_decoder, monkeypatch):
             lib.dsr_batch_destroy(h)
 
 
+@pytest.mark.parametrize("streams", ["1", "2"])
+def test_graph_replays_never_return_stale_records(gpu_decoder, monkeypatch, streams):
+    """Every replay poisons the out-records on the stream before its hipGraphLaunch and the
+    graph's k_finalize rewrites them; 150 replays, each downloaded at once, must all equal the
+    eager run — a download ordered before the graph's last kernel (or the poison after it)
+    would return the poison bytes.  ``streams`` 2: the captured two-group fork / join (round 3
+    saw an event recorded after a per-group graph launch fail to order later work, DESIGN
+    §3.5); 1: the graph mode's default one-group batch."""
+    from reconstruct import _libdsr as L
+
+    import bench
+
+    lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
+    params = L.optim_params(dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
+                                                                    num_iterations=2)))
+    monkeypatch.setenv("DSR_STREAMS", streams)
+    ref = None
+    for graph in ("0", "1"):
+        monkeypatch.setenv("DSR_GRAPH", graph)
+        h, keep = bench.make_batch(gpu_decoder, params, 8, 4100)
+        try:
+            for r in range(150 if graph == "1" else 1):
+                outs = (L.ObjectOut * 8)()
+                ctx.check(lib.dsr_batch_run(h), "run")
+                ctx.check(lib.dsr_batch_download(h, outs), "download")
+                if ref is None:
+                    ref = bytes(outs)
+                    assert all(o.is_good in (0, 1) for o in outs)
+                assert bytes(outs) == ref, f"replay {r} differs"
+        finally:
+            lib.dsr_batch_destroy(h)
+
+
 def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
     """The one-product classification pass + exact re-decode of the band (dsr_mlp_lite.hpp)
     vs decoding every sample exactly (DSR_LITE=0): same N_valid, K and step; and the pass's
