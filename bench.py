@@ -267,14 +267,14 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
-def fp32_algorithmic(a, steps, elapsed):
+def fp32_algorithmic(a, steps, elapsed, stats_steps=None):
     """SURVEY.md §8(d)'s algorithmic count: per object and iteration 2*1,769,984*(N + N_valid)
     + 2*1,835,520*(N + K) FLOP (fp32 decoder, every in-ball sample decoded, Jacobian points
     re-forwarded), summed over the timed steps, against the fp32 MFMA peak.  It exceeds that
     peak because the build decodes fewer samples (exact early ray termination), classifies most
     of them with one fp16 product and runs the rest as 3xFP16 — the fractions below."""
     n, nv, k = a.get("jac_surface_points", 0), a.get("inball_points", 0), a.get("jac_render_points", 0)
-    flop = 2.0 * FWD_MAC * (n + nv) + 2.0 * BWD_MAC * (n + k)
+    flop = (2.0 * FWD_MAC * (n + nv) + 2.0 * BWD_MAC * (n + k)) * steps / (stats_steps or steps)
     tf = flop / elapsed / 1e12 if elapsed > 0 else 0.0
     dec = a.get("fwd_points", 0)
     return {"flop_per_step": flop / max(1, steps), "achieved_tflops": round(tf, 1),
@@ -392,10 +392,15 @@ def main():
     n_good = 0
     gather_s = 0.0
     t0 = time.perf_counter()
+    # per-step kernel statistics (HIP-event times of every decoder launch, counters): read after
+    # every step at N = 1, where they feed the roofline; with several ranks only after the
+    # timed region, for the last step (~200 event queries + 3 copies per read, ~0.3 ms: 1% of
+    # an 8-object shard's step, which the strong-scaling value would otherwise carry)
+    per_step_stats = world == 1
     for _ in range(args.steps):
         res = shard.run()
         gather_s += shard.last_gather_s
-        if shard.handle is not None:
+        if shard.handle is not None and per_step_stats:
             st = L.Stats()
             ctx.check(lib.dsr_batch_stats(shard.handle, C.byref(st)), "stats")
             stats_sum(acc, st)
@@ -403,6 +408,12 @@ def main():
             n_good += sum(int(r["is_good"]) for r in res)
     barrier()
     elapsed = time.perf_counter() - t0
+    stats_steps = args.steps
+    if shard.handle is not None and not per_step_stats:
+        st = L.Stats()
+        ctx.check(lib.dsr_batch_stats(shard.handle, C.byref(st)), "stats")
+        stats_sum(acc, st)
+        stats_steps = 1
     per_rank = [elapsed]
     ranks = {"world_size": world, "shard_objects": [len(s) for s in shard.shards],
              "gather_ms_per_step": round(gather_s / args.steps * 1e3, 4)}
@@ -472,13 +483,14 @@ def main():
                 "max_observed_lite_error": acc["lite_max_err"], "min_margin": acc["lite_min_margin"]},
             "jac_points": {"surface": acc.get("jac_surface_points"), "render": acc.get("jac_render_points"),
                            "render_backward_only": bool(acc.get("keep_masks"))},
-            "fp32_algorithmic": fp32_algorithmic(acc, args.steps, elapsed) if acc else None,
+            "fp32_algorithmic": fp32_algorithmic(acc, args.steps, elapsed, stats_steps) if acc else None,
             "lite_broken_blocks": acc.get("lite_broken_blocks"),
             "test_hooks": acc.get("test_hooks"),
             "ranks": ranks,
             # device wall of one run (HIP events around dsr_batch_run's work, rank 0): the rest of
             # ms_per_step is host time (launch, download, packing, stats)
-            "device_ms_per_step": round(acc["total_ms"] / args.steps, 3) if acc else None,
+            "device_ms_per_step": round(acc["total_ms"] / stats_steps, 3) if acc else None,
+            "stats_steps": stats_steps,
             "good_fraction": n_good / float(n_job * args.steps),
             # inputs handed over in host memory: the upload added to one step
             "host_inclusive_value": n_job / (elapsed / args.steps + create_s),
