@@ -894,9 +894,10 @@ static int jac_variant() {
 }
 
 // dsr_batch_run: with DSR_GRAPH=1 the first run of a batch is enqueued eagerly and from
-// the second on (a re-run batch: streaming keyframes, config 5) the whole multi-stream
-// launch sequence — ~6 + 3 x passes launches per iteration and group — is captured once
-// into a hipGraph and replayed with one launch; dsr_batch_graph captures up front.  A
+// the second on (a re-run batch: streaming keyframes, config 5) the whole launch sequence —
+// ~6 + 3 x passes launches per iteration and object group; one group by default under
+// DSR_GRAPH=1 (batch_create_impl) — is captured once into a hipGraph and replayed with one
+// launch; dsr_batch_graph captures up front.  A
 // replayed run records only its total time (kernel events stay out of the graph: HIP
 // cannot time events recorded inside one), so dsr_batch_stats reports no kernel times.
 static bool graph_enabled() {        // DSR_GRAPH=1: replay re-run batches as hipGraphs
