@@ -1372,6 +1372,29 @@ int dsr_mesher_destroy(dsr_mesher* m) {
   return 0;
 }
 
+static bool mesher_alloc(dsr_mesher* m, void** p, size_t bytes) {
+  if (hipMalloc(p, std::max<size_t>(bytes, 4)) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  m->allocs.push_back(*p);
+  return true;
+}
+
+// The marching-cubes half of a mesher: the volume (tile-padded: the grid decode writes it) and
+// the edge / cell / scan / output buffers for m->d.
+static bool mesher_alloc_mc(dsr_mesher* m) {
+  const int d = m->d, n = m->n, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
+  const int nb = (std::max(ne, nc) + MC_SCAN_BLOCK - 1) / MC_SCAN_BLOCK;
+  auto A = [&](void** p, size_t bytes) { return mesher_alloc(m, p, bytes); };
+  return A((void**)&m->vol, sizeof(float) * (size_t)m->nt * TILE) &&
+         A((void**)&m->flag, sizeof(int) * (size_t)ne) && A((void**)&m->vidx, sizeof(int) * (size_t)ne) &&
+         A((void**)&m->ntri, sizeof(int) * (size_t)nc) && A((void**)&m->toff, sizeof(int) * (size_t)nc) &&
+         A((void**)&m->bsum, sizeof(int) * (size_t)nb) && A((void**)&m->tot, sizeof(int) * 2) &&
+         A((void**)&m->verts, sizeof(float) * 3 * (size_t)ne) &&
+         A((void**)&m->faces, sizeof(int) * 3 * (size_t)DSR_MC_MAX_TRI * nc);
+}
+
 int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pts, int vol_dim,
                       dsr_mesher** out) {
   if (!ctx || !dec || !grid_pts || !out) return fail(ctx, "null argument");
@@ -1384,22 +1407,12 @@ int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pt
   m->d = vol_dim;
   m->n = vol_dim * vol_dim * vol_dim;
   m->nt = (m->n + TILE - 1) / TILE;
-  const int d = vol_dim, n = m->n, nt = m->nt, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
-  const int nb = (std::max(ne, nc) + MC_SCAN_BLOCK - 1) / MC_SCAN_BLOCK;
-  auto A = [&](void** p, size_t bytes) {
-    if (hipMalloc(p, std::max<size_t>(bytes, 4)) != hipSuccess) return false;
-    m->allocs.push_back(*p);
-    return true;
-  };
+  const int n = m->n, nt = m->nt;
+  auto A = [&](void** p, size_t bytes) { return mesher_alloc(m, p, bytes); };
   if (!A((void**)&m->pts, sizeof(float4) * (size_t)nt * TILE) || !A((void**)&m->tiles, sizeof(Tile) * nt) ||
       !A((void**)&m->ntiles, sizeof(int)) || !A((void**)&m->desc, sizeof(ObjDesc)) ||
       !A((void**)&m->code, sizeof(float) * CODE) || !A((void**)&m->b0, sizeof(float) * HID) ||
-      !A((void**)&m->b4, sizeof(float) * HID) || !A((void**)&m->vol, sizeof(float) * (size_t)nt * TILE) ||
-      !A((void**)&m->flag, sizeof(int) * (size_t)ne) || !A((void**)&m->vidx, sizeof(int) * (size_t)ne) ||
-      !A((void**)&m->ntri, sizeof(int) * (size_t)nc) || !A((void**)&m->toff, sizeof(int) * (size_t)nc) ||
-      !A((void**)&m->bsum, sizeof(int) * (size_t)nb) || !A((void**)&m->tot, sizeof(int) * 2) ||
-      !A((void**)&m->verts, sizeof(float) * 3 * (size_t)ne) ||
-      !A((void**)&m->faces, sizeof(int) * 3 * (size_t)DSR_MC_MAX_TRI * nc)) {
+      !A((void**)&m->b4, sizeof(float) * HID) || !mesher_alloc_mc(m)) {
     dsr_mesher_destroy(m);
     return fail(ctx, "hipMalloc failed (mesher)");
   }
@@ -1431,13 +1444,15 @@ static void mc_scan(hipStream_t s, const int* in, int n, int* out, int* bsum, in
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(MC_SCAN_BLOCK), 0, s, in, n, (const int*)bsum, out);
 }
 
+static int mc_run(dsr_mesher* m, float level, float* verts, int vcap, int* faces, int fcap, int* n_verts,
+                  int* n_faces);
+
 int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, int vcap, int* faces,
                    int fcap, int* n_verts, int* n_faces) {
   if (!m || !code || !n_verts || !n_faces) return fail(m ? m->ctx : nullptr, "null argument");
   dsr_ctx* ctx = m->ctx;
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
-  const int d = m->d, n = m->n, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
   const DevDecoder& D = m->dec->D;
   DSR_CHECK(ctx, hipMemcpyAsync(m->code, code, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)m->code, m->b0, m->b4);
@@ -1445,6 +1460,15 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
                      ErtArgs{nullptr, 1, 0.f, nullptr, nullptr}, MaskArgs{nullptr, nullptr, nullptr, nullptr});
+  return mc_run(m, level, verts, vcap, faces, fcap, n_verts, n_faces);
+}
+
+// Marching cubes over m->vol (already on m's context stream) and the copy-out.
+static int mc_run(dsr_mesher* m, float level, float* verts, int vcap, int* faces, int fcap, int* n_verts,
+                  int* n_faces) {
+  dsr_ctx* ctx = m->ctx;
+  hipStream_t s = ctx->stream;
+  const int d = m->d, n = m->n, nc = (d - 1) * (d - 1) * (d - 1), ne = 3 * n;
   const int B = 256;
   hipLaunchKernelGGL(k_mc_edges, dim3((n + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->flag);
   hipLaunchKernelGGL(k_mc_cells, dim3((nc + B - 1) / B), dim3(B), 0, s, (const float*)m->vol, d, level, m->ntri);
@@ -1467,6 +1491,28 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   if (tot[0] > 0) DSR_CHECK(ctx, hipMemcpy(verts, m->verts, sizeof(float) * 3 * tot[0], hipMemcpyDeviceToHost));
   if (tot[1] > 0) DSR_CHECK(ctx, hipMemcpy(faces, m->faces, sizeof(int) * 3 * tot[1], hipMemcpyDeviceToHost));
   return 0;
+}
+
+int dsr_mc_volume(dsr_ctx* ctx, const float* vol, int vol_dim, float level, float* verts, int vcap, int* faces,
+                  int fcap, int* n_verts, int* n_faces) {
+  if (!ctx || !vol || !n_verts || !n_faces) return fail(ctx, "null argument");
+  if (vol_dim < 2 || vol_dim > 512) return fail(ctx, "vol_dim must be in [2, 512]");
+  hipSetDevice(ctx->device);
+  dsr_mesher m;
+  m.ctx = ctx;
+  m.d = vol_dim;
+  m.n = vol_dim * vol_dim * vol_dim;
+  m.nt = (m.n + TILE - 1) / TILE;
+  struct Free {       // the scratch lives for this call only
+    dsr_mesher* m;
+    ~Free() {
+      hipStreamSynchronize(m->ctx->stream);
+      for (void* p : m->allocs) hipFree(p);
+    }
+  } guard{&m};
+  if (!mesher_alloc_mc(&m)) return fail(ctx, "hipMalloc failed (marching cubes)");
+  DSR_CHECK(ctx, hipMemcpyAsync(m.vol, vol, sizeof(float) * (size_t)m.n, hipMemcpyHostToDevice, ctx->stream));
+  return mc_run(&m, level, verts, vcap, faces, fcap, n_verts, n_faces);
 }
 
 int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts, int n,

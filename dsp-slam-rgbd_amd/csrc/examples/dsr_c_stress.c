@@ -13,7 +13,8 @@
  *                              graph capture + replays (DSR_GRAPH=1), multi-context
  *                              reconstruct_multi, sdf_eval with and without the Jacobian,
  *                              pose-only single and batched (including an empty object), the
- *                              mesher with ample and with too small capacities, forced audit
+ *                              mesher (and dsr_mc_volume on its decoded grid) with ample and
+ *                              with too small capacities, forced audit
  *                              violations and their spare-iteration redo (test hooks), and the
  *                              error paths of a live context.  Exit status 0 = every check held.
  */
@@ -353,6 +354,20 @@ int main(int argc, char** argv) {
     CHECK(dsr_mesher_run(m, ref[0].code, 0.f, V, 1, F, 1, &nv2, &nf2) == -5, "small capacity accepted");
     CHECK(nv2 == nvert && nf2 == nface, "counts on -5");
     CHECK(dsr_mesher_destroy(m) == 0, "mesher_destroy");
+    /* the same grid decoded by dsr_sdf_eval, meshed by dsr_mc_volume: the mesher's mesh */
+    float* vol = (float*)malloc(sizeof(float) * nv);
+    float* V2 = (float*)malloc(sizeof(float) * 3 * (size_t)vcap);
+    int* F2 = (int*)malloc(sizeof(int) * 3 * (size_t)fcap);
+    CHECK(dsr_sdf_eval(ctx, dec, ref[0].code, grid, (int)nv, vol, NULL) == 0, "%s", dsr_last_error(ctx));
+    nv2 = nf2 = -1;
+    CHECK(dsr_mc_volume(ctx, vol, d, 0.f, V2, vcap, F2, fcap, &nv2, &nf2) == 0, "%s", dsr_last_error(ctx));
+    CHECK(nv2 == nvert && nf2 == nface, "mc_volume counts %d/%d vs %d/%d", nv2, nf2, nvert, nface);
+    CHECK(memcmp(V, V2, sizeof(float) * 3 * (size_t)nvert) == 0 && memcmp(F, F2, sizeof(int) * 3 * (size_t)nface) == 0,
+          "mc_volume mesh differs from the mesher's");
+    CHECK(dsr_mc_volume(ctx, vol, d, 0.f, V2, 1, F2, 1, &nv2, &nf2) == -5 && nv2 == nvert, "mc_volume small capacity");
+    CHECK(dsr_mc_volume(ctx, NULL, d, 0.f, V2, vcap, F2, fcap, &nv2, &nf2) < 0, "mc_volume without volume");
+    CHECK(dsr_mc_volume(ctx, vol, 1, 0.f, V2, vcap, F2, fcap, &nv2, &nf2) < 0, "mc_volume vol_dim 1 accepted");
+    free(vol); free(V2); free(F2);
     free(grid); free(V); free(F);
   }
 

@@ -67,7 +67,7 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 6          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 7          # include/dsr.h DSR_ABI_VERSION
 
 
 class Stats(C.Structure):
@@ -124,6 +124,7 @@ SIGNATURES = {
     "dsr_mesher_create": (C.c_int, [C.c_void_p, C.c_void_p, FP, C.c_int, C.POINTER(C.c_void_p)]),
     "dsr_mesher_run": (C.c_int, [C.c_void_p, FP, C.c_float, FP, C.c_int, IP, C.c_int, IP, IP]),
     "dsr_mesher_destroy": (C.c_int, [C.c_void_p]),
+    "dsr_mc_volume": (C.c_int, [C.c_void_p, FP, C.c_int, C.c_float, FP, C.c_int, IP, C.c_int, IP, IP]),
 }
 
 _lib = None

@@ -1,15 +1,39 @@
-"""Config / decoder factory half of ``reconstruct/utils.py`` (utils.py:58-116).
+"""``reconstruct/utils.py`` of the reference, every public name (utils.py:26-161).
 
 Same names and behaviour the C++ side relies on (src/System.cc:95-98):
 ``get_configs(path)`` returns an attribute dict that raises ``KeyError`` on a
 missing key (``ForceKeyErrorDict``, utils.py:82-90), ``get_decoder(cfg)`` returns
-the decoder handle built from ``cfg.DeepSDF_DIR`` (utils.py:93-94).
+the decoder handle built from ``cfg.DeepSDF_DIR`` (utils.py:93-94).  The mesher half
+(``create_voxel_grid``, ``convert_sdf_voxels_to_mesh``, ``write_mesh_to_ply``) and the
+viewer helpers the reference's scripts import (``color_table``, ``set_view``:
+reconstruct_frame.py:20, visualize_map.py:22) keep their names too.
 """
 from __future__ import annotations
 
 import json
 
 import numpy as np
+
+
+# the reference's visualisation palette (utils.py:26-37), RGB in [0, 1]: red, green, blue,
+# magenta, orange, purple, cyan, lime, pink, teal
+color_table = [[r / 255., g / 255., b / 255.] for r, g, b in (
+    (230, 0, 0), (60, 180, 75), (0, 0, 255), (255, 0, 255), (255, 165, 0),
+    (128, 0, 128), (0, 255, 255), (210, 245, 60), (250, 190, 190), (0, 128, 128))]
+
+
+def set_view(vis, dist=100., theta=np.pi / 6.):
+    """utils.py:40-55: point an Open3D visualiser's camera at the world origin from `dist`
+    along its z axis, tilted by `theta` about x (world -> eye extrinsic).  Needs only the
+    visualiser object the caller passes (no open3d import here)."""
+    ctl = vis.get_view_control()
+    cam = ctl.convert_to_pinhole_camera_parameters()
+    c, s = np.cos(theta), np.sin(theta)
+    cam.extrinsic = np.array([[1., 0., 0., 0.],
+                              [0., c, -s, 0.],
+                              [0., s, c, dist],
+                              [0., 0., 0., 1.]])
+    ctl.convert_from_pinhole_camera_parameters(cam)
 
 
 class ForceKeyErrorDict(dict):
@@ -97,6 +121,33 @@ def create_voxel_grid(vol_dim=128):
     values[:, 2] = values[:, 2] * np.float32(voxel_size) + np.float32(voxel_origin[0])
     return values
 
+
+def convert_sdf_voxels_to_mesh(pytorch_3d_sdf_tensor, level=0.0, device=None):
+    """utils.py:119-140 on device (``dsr_mc_volume``): marching cubes of an (n, n, n) SDF
+    volume (torch tensor or array, C order — the grid order of ``create_voxel_grid``), vertices
+    as voxel index x 2/(n-1) - 1 (the reference's spacing and origin shift), faces as vertex
+    indices.  Returns (vertices float32 (V, 3), faces int32 (F, 3)) — float32 because the
+    build's only caller, ``MeshExtractor``, casts to it anyway (optimizer.py:228).  The
+    triangulation is the build's marching cubes, not skimage's ``marching_cubes_lewiner``
+    (absent here: parity unpinned)."""
+    import ctypes as C
+
+    from reconstruct import _libdsr as L
+
+    t = pytorch_3d_sdf_tensor
+    if hasattr(t, "detach"):
+        t = t.detach().cpu().numpy()
+    vol = np.ascontiguousarray(t, dtype=np.float32)
+    if vol.ndim != 3 or len(set(vol.shape)) != 1:
+        raise ValueError(f"expected an (n, n, n) volume, got shape {vol.shape}")
+    d = vol.shape[0]
+    ctx = L.Context.get(device)
+    verts = np.zeros((3 * d ** 3, 3), np.float32)
+    faces = np.zeros((5 * (d - 1) ** 3, 3), np.int32)
+    nv, nf = C.c_int(), C.c_int()
+    ctx.check(ctx.lib.dsr_mc_volume(ctx.handle, L.fptr(vol), d, float(level), L.fptr(verts), verts.shape[0],
+                                    L.iptr(faces), faces.shape[0], C.byref(nv), C.byref(nf)), "dsr_mc_volume")
+    return verts[:nv.value].copy(), faces[:nf.value].copy()
 
 
 # PLY layout plyfile.PlyData([vertex(x,y,z f4), face(vertex_indices i4 x3)]).write() produces

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 6
+#define DSR_ABI_VERSION 7
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -214,6 +214,15 @@ int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pt
 int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, int vcap, int* faces,
                    int fcap, int* n_verts, int* n_faces);
 int dsr_mesher_destroy(dsr_mesher* m);
+
+/* ---- marching cubes on a caller's volume: replaces convert_sdf_voxels_to_mesh
+ * (utils.py:119-140) called on its own.  `vol` is the (vol_dim, vol_dim, vol_dim) SDF
+ * volume in C order (vol[(i*vol_dim + j)*vol_dim + k] at voxel (i, j, k), the order
+ * MeshExtractor's grid decode produces it in); vertices come back as voxel index x 2/(vol_dim-1)
+ * - 1 (the reference's spacing and origin shift), faces as vertex indices.  Same kernels,
+ * capacities and -5 status as dsr_mesher_run; device scratch lives for the call only. */
+int dsr_mc_volume(dsr_ctx* ctx, const float* vol, int vol_dim, float level, float* verts, int vcap,
+                  int* faces, int fcap, int* n_verts, int* n_faces);
 
 /* ---- multi-GPU from one process: replaces the per-detection loop
  * LocalMapping_util.cc:165-206 spread over devices.  ctx[g] / dec[g] are one context and

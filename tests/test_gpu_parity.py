@@ -469,6 +469,39 @@ def test_mesh_extractor_matches_oracle_and_level_set(gpu_decoder):
         assert np.median(np.abs(s)) < 0.02 * h and np.abs(s).max() < 0.5 * h
 
 
+def test_convert_sdf_voxels_to_mesh_on_a_caller_volume(gpu_decoder):
+    """convert_sdf_voxels_to_mesh (utils.py:119-140) called on its own (dsr_mc_volume): on the
+    MeshExtractor's decoded grid it returns exactly MeshExtractor's mesh; on analytic volumes
+    (a sphere, a torus, as torch tensor and ndarray, odd sizes, a level other than 0, a volume
+    without a crossing) exactly the CPU restatement's (oracle/dsr_mc.py).  (Against skimage's
+    marching_cubes_lewiner: parity unpinned.)"""
+    import torch
+
+    from oracle.dsr_mc import marching_cubes
+    from reconstruct.optimizer import MeshExtractor
+    from reconstruct.utils import convert_sdf_voxels_to_mesh
+
+    ex = MeshExtractor(gpu_decoder, 64, 40)
+    code = (0.3 * np.random.default_rng(5).standard_normal(64)).astype(np.float32)
+    m = ex.extract_mesh_from_code(code)
+    v, f = convert_sdf_voxels_to_mesh(torch.from_numpy(ex.decode_grid(code).reshape(40, 40, 40)))
+    assert v.dtype == np.float32 and f.dtype == np.int32
+    assert np.array_equal(v, m.vertices) and np.array_equal(f, m.faces) and f.shape[0] > 500
+    for d, level in ((33, 0.0), (17, 0.05), (2, 0.0)):
+        g = np.linspace(-1.0, 1.0, d)
+        x, y, z = np.meshgrid(g, g, g, indexing="ij")
+        sphere = (np.sqrt(x * x + y * y + z * z) - 0.6).astype(np.float32)
+        torus = (np.sqrt((np.sqrt(x * x + y * y) - 0.55) ** 2 + z * z) - 0.25).astype(np.float32)
+        for vol in (sphere, torus):
+            gv, gf = convert_sdf_voxels_to_mesh(vol, level=level)
+            ov, of = marching_cubes(vol, level)
+            assert np.array_equal(gv, ov) and np.array_equal(gf, of), (d, level)
+    v, f = convert_sdf_voxels_to_mesh(np.ones((9, 9, 9), np.float32))
+    assert v.shape == (0, 3) and f.shape == (0, 3)
+    with pytest.raises(ValueError):
+        convert_sdf_voxels_to_mesh(np.ones((4, 4, 5), np.float32))
+
+
 def test_extract_map_objects_end_to_end(gpu_decoder, tmp_path):
     """MapObjects.txt -> objects/<id>.npy + .ply (extract_map_objects.py:46-63) on device."""
     from reconstruct.map_objects import extract_map_objects, write_map_objects

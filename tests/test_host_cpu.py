@@ -183,6 +183,40 @@ def test_vertex_transform_matches_reference_f9():
     assert np.allclose(f["spacing"], 2.0 / (int(f["dim"]) - 1)) and float(f["level"]) == 0.0
 
 
+def test_viewer_helpers_match_reference_f11():
+    """color_table / set_view (utils.py:26-55), imported by the reference's scripts
+    (reconstruct_frame.py:20, visualize_map.py:22): the palette and the extrinsic set_view
+    installs, against golden F11 (tests/golden/make_utils.py, recorded from the reference)."""
+    import types
+
+    from reconstruct.utils import color_table, set_view
+
+    f = golden("f11_utils.npz")
+    assert np.array_equal(np.asarray(color_table, np.float64), f["color_table"])
+
+    class Vis:
+        installed = None
+
+        def get_view_control(self):
+            vis = self
+
+            class Ctl:
+                def convert_to_pinhole_camera_parameters(self):
+                    return types.SimpleNamespace(extrinsic=np.zeros((4, 4)))
+
+                def convert_from_pinhole_camera_parameters(self, cam):
+                    vis.installed = np.array(cam.extrinsic, np.float64)
+            return Ctl()
+
+    for (dist, theta), ext in zip(f["views"], f["extrinsics"][:-1]):
+        v = Vis()
+        set_view(v, dist=float(dist), theta=float(theta))
+        assert np.array_equal(v.installed, ext)
+    v = Vis()
+    set_view(v)
+    assert np.array_equal(v.installed, f["extrinsics"][-1])
+
+
 def test_grid_decode_order_matches_reference_f9(oracle_dec):
     """The reference decodes create_voxel_grid's points and views them as (d, d, d)
     (optimizer.py:225-227): the oracle's decode in the same order reproduces the volume."""
