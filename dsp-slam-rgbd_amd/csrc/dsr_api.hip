@@ -611,8 +611,10 @@ static hipError_t pool_event(dsr_ctx* ctx, hipEvent_t* e, bool timing) {
 }
 
 // Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
-// (1.0): out-of-band samples with |y| < th + shell*margin are audited; DSR_LITE_AUDIT_LOG2
-// (7): plus a hashed 2^-log2 share of all other decoded samples; DSR_LITE_PERTURB: test hook
+// (1.0): out-of-band samples with |y| < th + (1 + shell)*margin — `shell` margins beyond the
+// band edge — are audited; DSR_LITE_AUDIT_LOG2 (7): plus a hashed 2^-log2 share of all other
+// decoded samples (0: all of them — the audit-everything survey, tools/lite_audit_all.py);
+// DSR_LITE_PERTURB: test hook
 static ErtArgs lite_settings(bool hooks) {
   auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
   ErtArgs E{};

@@ -107,7 +107,8 @@ struct ErtArgs {
   unsigned char* refine; // lite pass: [sum n_rays*M] samples to decode exactly
   int lag;               // staggered lite pass: k step at which group B may start a GEMM
   // lite-pass audit (dsr_mlp_lite.hpp: lite_flag): out-of-band samples with |y| < th +
-  // shell*margin, and a hashed 2^-audit_log2 share of all others, are re-decoded exactly too
+  // (1 + shell)*margin — the band edge plus `shell` margins — and a hashed 2^-audit_log2 share
+  // of all others (audit_log2 = 0: every sample) are re-decoded exactly too
   int audit;             // 0: no audit
   float shell;
   int audit_log2;
@@ -143,8 +144,8 @@ __device__ __forceinline__ unsigned char lite_flag(const ErtArgs& E, float y, in
   full = y <= E.nth - margin;
   if (!E.audit) return 0;
   const unsigned h = (unsigned)(idx ^ (salt * 0x5bd1e995)) * 2654435761u;
-  const bool au = fabsf(y) < -E.nth + E.shell * margin ||
-                  (E.audit_log2 > 0 && (h >> (32 - E.audit_log2)) == 0u);
+  const bool au = fabsf(y) < -E.nth + (1.f + E.shell) * margin ||
+                  E.audit_log2 == 0 || (h >> (32 - E.audit_log2)) == 0u;
   return au ? (full ? 3 : 2) : 0;
 }
 
