@@ -106,6 +106,29 @@ def test_audit_guard_fires_and_redoes_exactly(gpu_decoder, monkeypatch):
     assert any(int(t2[i]["k"][0]) != int(t0[i]["k"][0]) for i in range(len(objs)))
 
 
+def test_audit_shell_catches_with_certainty(gpu_decoder, monkeypatch):
+    """The certain part of the audit alone (hashed share 2^-24: practically none): lite values
+    perturbed by +-0.015 push band samples (|sdf| < th = 0.01, first-iteration margin m = 0.01)
+    into th+m..th+2m, the shell, which is re-decoded whatever the hash says — every object sees
+    violations and is redone.  With the shell off (DSR_LITE_SHELL=0, the shipped behaviour
+    before round 3's fix: the shell sat on the band edge) the same run audits almost nothing."""
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=1)
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
+            for e in (0, 4, 9)]
+    monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
+    monkeypatch.setenv("DSR_LITE_PERTURB", "0.015")
+    monkeypatch.setenv("DSR_LITE_AUDIT_LOG2", "24")
+    outs, st = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert st.lite_audit_violations > 0 and st.lite_redo_objects == len(objs)
+    assert all(outs[i].is_good and outs[i].iters_done == 1 for i in range(len(objs)))
+    monkeypatch.setenv("DSR_LITE_SHELL", "0")
+    _, st0 = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert st0.audit_points < 0.01 * st.audit_points, (st0.audit_points, st.audit_points)
+    assert st0.lite_audit_violations < st.lite_audit_violations
+
+
 def test_audit_quiet_and_cheap_on_the_bench_workload(gpu_decoder, monkeypatch):
     """Unperturbed: no violation, the audit re-decodes a bounded share of the samples."""
     monkeypatch.setenv("DSR_LITE", "1")
