@@ -636,7 +636,7 @@ static GNParams make_params(const dsr_optim_params* p) {
   auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
   // lite-pass margin: th in the first iteration, then max(0.002, 4 x the
   // largest |lite - exact| the object's band and audit samples showed; the audit guards it)
-  P.lite_margin0 = envf("DSR_LITE_MARGIN", 0.01f);
+  P.lite_margin0 = envf("DSR_LITE_MARGIN", p->cut_off);     // th (0.01 in every reference config)
   P.lite_floor = envf("DSR_LITE_FLOOR", 0.002f);
   P.lite_safety = envf("DSR_LITE_SAFETY", 4.0f);
   return P;
