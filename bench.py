@@ -16,8 +16,10 @@ config 4 (64 objects x 4096 points, 8 per GPU at N=8).
 Inputs are resident in HBM before the timed region (dsr_batch_create); each step
 re-initialises the optimizer state on device and runs all iterations.  At N=1 rank 0
 also reports: the exact-decode leg (``value_exact``: DSR_LITE=0, every ray sample
-decoded in 3xFP16), the three MFMA kernels' rooflines, the CPU baseline, and the
-Redwood keyframe leg (BASELINE config 5, ``keyframe``).
+decoded in 3xFP16), the three MFMA kernels' rooflines, the CPU baseline, the
+Redwood keyframe leg (BASELINE config 5, ``keyframe``), one 16-object KITTI frame as one batch
+(config 3 of the list, ``config2_frame``) and one object per ``reconstruct_object`` call
+(``config1_single``).
 
 Every N also runs a ``config4`` leg: BASELINE config 4 (64 objects x 4096 points, the same
 LPT sharding, 8 per GPU at N=8), so one N=1,2,4,8 sweep gives both strong-scaling curves.
@@ -320,6 +322,39 @@ def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_
         shard.close()
 
 
+def small_legs(opt, objs, steps=3):
+    """BASELINE configs[2] and configs[1] taken literally, beside the 64-object metric job:
+    one KITTI frame of 16 objects x 2048 pts as one resident batch (obj/s), and ONE object per
+    call through the reference's own entry point, ``Optimizer.reconstruct_object``
+    (LocalMapping_util.cc:181-194 calls it once per detection): ms per call, uploads and
+    download included."""
+    import torch
+    from reconstruct.parallel import ResidentShard
+
+    sh = ResidentShard(opt, objs[:16])
+    try:
+        sh.run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sh.run()
+        dt = time.perf_counter() - t0
+    finally:
+        sh.close()
+    o = objs[0]
+    opt.reconstruct_object(*o[:4])                      # warm-up (pooled buffers, events)
+    t1 = time.perf_counter()
+    for _ in range(5):
+        r = opt.reconstruct_object(*o[:4])
+    single = (time.perf_counter() - t1) / 5
+    return {"config2_frame": {"objects": 16, "value": 16 * steps / dt, "unit": "object-reconstructions/sec",
+                              "ms_per_frame": dt / steps * 1e3,
+                              "note": "BASELINE configs[2]: one KITTI frame of 16 x 2048-pt objects, one batch"},
+            "config1_single": {"ms_per_call": single * 1e3, "is_good": bool(r.is_good),
+                               "note": "BASELINE configs[1]: one 2048-pt object, 10 GN iters, per "
+                                       "Optimizer.reconstruct_object call (H2D + run + D2H)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -537,6 +572,7 @@ def main():
                                                                    "avg_launch_ms", "launches")}
                                        for name, e in r1.items()}
         out["keyframe"] = keyframe_leg(dec)
+        out.update(small_legs(opt, objs))
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_pts=args.pts)
