@@ -138,6 +138,7 @@ def _ks_p(a, b):
 
 @pytest.mark.parametrize("name,optim,dtp,mode", [("kitti0", S.KITTI_OPTIM, "KITTI", "distribution"),
                                                  ("kitti5", S.KITTI_OPTIM, "KITTI", "distribution"),
+                                                 ("kitti4096", S.KITTI_OPTIM, "KITTI", "distribution"),
                                                  ("redwood0", S.REDWOOD_OPTIM, "Redwood", "support"),
                                                  ("redwood1", S.REDWOOD_OPTIM, "Redwood", "support")])
 def test_full_size_ensemble_matches_reference_ensemble(gpu_decoder, name, optim, dtp, mode):
@@ -163,8 +164,11 @@ def test_full_size_ensemble_matches_reference_ensemble(gpu_decoder, name, optim,
     Redwood check is that the GPU cloud lies inside the reference's: its final losses within the
     reference members' range widened by a quarter of that range on each side, its largest
     pose / code deviation from the unperturbed result within 1.25x the reference members'
-    largest, its 90th percentile within 1.5x theirs."""
-    f = golden(f"f4_traj_{name}.npz")
+    largest, its 90th percentile within 1.5x theirs.
+
+    kitti4096: BASELINE config 4's object (4096 pts x 4296 rays, 10 iterations; golden F12,
+    tests/golden/make_ens4096.py), in the KITTI mode."""
+    f = golden("f12_ens_kitti4096.npz" if name == "kitti4096" else f"f4_traj_{name}.npz")
     t_init = f[ENS + "t_init"]
     n = t_init.shape[0]
     from reconstruct.optimizer import Optimizer
