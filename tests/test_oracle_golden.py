@@ -6,6 +6,8 @@ trusted as the checker of the HIP path.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -141,6 +143,25 @@ def test_reference_spread_fixture_is_consistent():
         f = golden(f"f4_traj_{name}.npz")
         assert f["ens_loss"].shape[0] >= 4
         assert np.isfinite(f["ens_loss"]).all()
+
+
+def test_config4_ensemble_fixture_is_consistent():
+    """F12 (tests/golden/make_ens4096.py): the F4 4096-point object at the full 10 iterations, the
+    members' starts are the shared ulp-perturbation generator's, every member and the unperturbed
+    run are good, and the unperturbed loss sits inside the members' spread."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_ensemble import member_poses
+
+    f = golden("f12_ens_kitti4096.npz")
+    f4 = golden("f4_traj_kitti4096.npz")
+    assert np.array_equal(f["obj_pts"], f4["obj_pts"]) and int(f["num_iterations"]) == 10
+    assert f["obj_pts"].shape == (4096, 3) and f["obj_rays"].shape == (4296, 3)
+    assert np.array_equal(f["ens64_t_init"], member_poses(f["obj_t_cam_obj"], 64))
+    assert bool(f["is_good"]) and bool(np.all(f["ens64_is_good"]))
+    lo, hi = f["ens64_loss"].min(), f["ens64_loss"].max()
+    assert lo <= float(f["loss"]) <= hi and hi - lo < 0.05 * float(f["loss"])
 
 
 def test_failure_semantics():
