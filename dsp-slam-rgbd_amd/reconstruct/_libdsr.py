@@ -128,7 +128,7 @@ SIGNATURES = {
 }
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()       # re-entrant: Context.get holds it while load_library takes it
 
 
 def lib_path() -> str:
@@ -189,9 +189,10 @@ class Context:
     def get(cls, device: int | None = None) -> "Context":
         if device is None:
             device = int(os.environ.get("DSR_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-        if device not in cls._cache:
-            cls._cache[device] = Context(device)
-        return cls._cache[device]
+        with _lock:            # one context per device even when threads race to create it
+            if device not in cls._cache:
+                cls._cache[device] = Context(device)
+            return cls._cache[device]
 
     def check(self, rc: int, what: str):
         if rc != 0:

@@ -1,0 +1,48 @@
+"""One object per Optimizer.reconstruct_object call — the reference's per-detection pattern
+(LocalMapping_util.cc:181-194) — timed back to back (GPU box).
+
+Usage: python tools/single_call.py [--reps N] [--pts P]    -> ms per call (median, min)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "dsp-slam-rgbd_amd"))
+sys.path.insert(0, REPO)
+
+import synthetic as S  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--pts", type=int, default=2048)
+    a = ap.parse_args()
+    from deep_sdf.workspace import decoder_from_state
+    from reconstruct.optimizer import Optimizer
+    from reconstruct.utils import ForceKeyErrorDict
+
+    dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS, device=0)
+    opt = Optimizer(dec, ForceKeyErrorDict(data_type="KITTI", optimizer=S.KITTI_OPTIM))
+    objs = [S.kitti_object(i, n_pts=a.pts) for i in range(4)]
+    opt.reconstruct_object(objs[0].t_cam_obj, objs[0].pts, objs[0].rays, objs[0].depth)
+    ts = []
+    for r in range(a.reps):
+        o = objs[r % 4]
+        t0 = time.perf_counter()
+        res = opt.reconstruct_object(o.t_cam_obj, o.pts, o.rays, o.depth)
+        ts.append(time.perf_counter() - t0)
+        assert res.is_good
+    ts = np.array(ts) * 1e3
+    print(f"single reconstruct_object ({a.pts} pts, 10 iters): median {np.median(ts):.3f} ms, "
+          f"min {ts.min():.3f} ms over {a.reps} calls", flush=True)
+
+
+if __name__ == "__main__":
+    main()
