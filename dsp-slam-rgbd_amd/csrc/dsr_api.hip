@@ -553,10 +553,14 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // fill the chip: each pass costs at least one tile's latency, extra samples are nearly free
 // (measured: 64 KITTI objects 186 vs 176 obj/s, 8 Redwood objects 10.6 vs 11.2 ms per
 // batch; round 2, same box: 8 KITTI objects 341-346 obj/s with 16,24 vs 337-341 with
-// 8,16,24, keyframe batch 4.82 vs 4.98 ms).
+// 8,16,24, keyframe batch 4.82 vs 4.98 ms).  Below 100k ray samples (one or two Redwood
+// objects: the reference's one-call-per-detection pattern) one pass: its tiles fit one round of
+// the chip, so every extra pass is a whole tile latency plus a sample pass (round 3, one box: a
+// Redwood object per reconstruct_object call 4.1 -> 3.1 ms; a KITTI object, 112k samples, 9.8 ms
+// either way; the 8-hypothesis keyframe batch 4.90 ms with 16,24 vs 5.90 with one pass).
 static std::vector<int> render_passes(int M, long samples) {
   const char* e = getenv("DSR_RENDER_PASSES");
-  std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : "16,24");
+  std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : samples >= 100000 ? "16,24" : "0");
   std::vector<int> r{0};
   size_t p = 0;
   while (p < spec.size()) {
