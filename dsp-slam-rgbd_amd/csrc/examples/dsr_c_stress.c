@@ -81,6 +81,11 @@ static void no_device_paths(void) {
         "batch calls on NULL accepted");
   CHECK(dsr_batch_download(NULL, NULL) < 0 && dsr_batch_stats(NULL, NULL) < 0, "batch NULL accepted");
   CHECK(dsr_mesher_destroy(NULL) == 0, "mesher_destroy(NULL)");
+  {
+    float v[8] = {0};
+    int nv = 0, nf = 0;
+    CHECK(dsr_mc_volume(NULL, v, 2, 0.f, NULL, 0, NULL, 0, &nv, &nf) < 0, "mc_volume(NULL ctx) accepted");
+  }
   dsr_ctx* c = NULL;
   const int rc2 = dsr_ctx_create(-7, &c);
   CHECK(rc2 < 0 && c == NULL, "ctx_create(-7) = %d", rc2);
