@@ -376,7 +376,7 @@ def test_c_stress_leaks_nothing_beyond_the_runtime(gpu_decoder, tmp_path):
     allocations from context creation on, made through libstdc++'s operator new, whose frames
     the sanitizer cannot attribute.  So the run with every section of the stress driver
     (resident batches, pool re-use, traces, reconstruct_multi's threads, queries, mesher, pose
-    batches, error paths) must leave exactly the allocations the run with none of them
+    batches, error paths) must leave no more allocations than the run with none of them
     leaves: a batch, event, pool block or thread record of libdsr that is never freed would
     add to them.  Graph capture is left out of both: HIP's graph implementation keeps ~43 MB
     and 9 unattributed allocations after hipGraphExecDestroy / hipGraphDestroy
@@ -396,7 +396,10 @@ def test_c_stress_leaks_nothing_beyond_the_runtime(gpu_decoder, tmp_path):
 
     every = leaked("graph")
     none = leaked("graph,trace,resident,redo,multi,query,mesher,errors")
-    assert every == none, (every, none)
+    # the same number of unattributed runtime allocations, and no more bytes beyond a few
+    # dozen: the runtime's own blocks vary by a few bytes with the path taken (DSR_STREAMS=1:
+    # 6,648 B with every section vs 6,672 B with none, 116 allocations both)
+    assert every[1] <= none[1] and every[0] <= none[0] + 64, (every, none)
 
 
 def test_replicated_object_matches_the_original(gpu_decoder):
