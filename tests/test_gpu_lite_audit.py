@@ -129,6 +129,22 @@ def test_audit_shell_catches_with_certainty(gpu_decoder, monkeypatch):
     assert st0.lite_audit_violations < st.lite_audit_violations
 
 
+def test_audit_everything_mode(gpu_decoder, monkeypatch):
+    """DSR_LITE_AUDIT_LOG2=0 (tools/lite_audit_all.py): every sample the lite pass decoded up to
+    its ray's first certainly-full one is re-decoded exactly — band samples as band, all others
+    as audits — and no class differs.  (Samples behind that one, decoded because they share its
+    pass window, are not: transmittance is exactly 0 there, §3.3; ~9% of the lite samples.)"""
+    monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.setenv("DSR_LITE_AUDIT_LOG2", "0")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=3)
+    objs = [S.kitti_object(i) for i in range(4)]
+    outs, st = batch_stats(opt, [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in objs])
+    assert all(outs[i].is_good for i in range(len(objs)))
+    assert st.lite_audit_violations == 0 and st.lite_redo_objects == 0
+    assert 0.8 * st.fwd_points <= st.refine_points <= st.fwd_points, (st.refine_points, st.fwd_points)
+    assert st.audit_points > 0.5 * st.fwd_points
+
+
 def test_audit_quiet_and_cheap_on_the_bench_workload(gpu_decoder, monkeypatch):
     """Unperturbed: no violation, the audit re-decodes a bounded share of the samples."""
     monkeypatch.setenv("DSR_LITE", "1")

@@ -2,7 +2,8 @@
 on full GN trajectories instead of emulated (tools/lite_error_survey.py is the numpy emulation).
 
 With DSR_LITE_AUDIT_LOG2=0 the audit's hashed share is 2^0: the exact split-fp16 pass re-decodes
-EVERY sample the lite pass decoded, records |lite - exact| (dsr_stats.lite_max_err) and compares
+every sample the lite pass decoded up to its ray's first certainly-full one (the ones behind it sit
+at transmittance 0 and cannot affect an output), records |lite - exact| (dsr_stats.lite_max_err) and compares
 the two classes (full <= -th | band | empty >= th) outside the band (lite_audit_violations; a
 violation discards that object's iteration and redoes it exactly).  Run over decoders of three
 hidden-weight gains, warm-start codes of three scales and 64 KITTI objects x 10 iterations, at
