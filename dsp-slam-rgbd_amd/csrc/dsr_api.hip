@@ -558,9 +558,14 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // the chip, so every extra pass is a whole tile latency plus a sample pass (round 3, one box: a
 // Redwood object per reconstruct_object call 4.1 -> 3.1 ms; a KITTI object, 112k samples, 9.8 ms
 // either way; the 8-hypothesis keyframe batch 4.90 ms with 16,24 vs 5.90 with one pass).
-static std::vector<int> render_passes(int M, long samples) {
+// A batch whose first 16-rank window would spill just past one round of lite tiles (n_cu
+// 128-point tiles: one KITTI-sized object per call) gets a first window that fits that round.
+static std::vector<int> render_passes(int M, long samples, long rays, int n_cu) {
   const char* e = getenv("DSR_RENDER_PASSES");
   std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : samples >= 100000 ? "16,24" : "0");
+  const long round = (long)n_cu * LTILE;
+  if (!e && spec == "16,24" && rays > 0 && rays * 16 > round && rays * 12 <= round)
+    spec = std::to_string(round / rays) + ",24";
   std::vector<int> r{0};
   size_t p = 0;
   while (p < spec.size()) {
@@ -871,7 +876,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     hipMemsetAsync(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj, ctx->stream);
     hipMemsetAsync(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj, ctx->stream);
   }
-  b->passes = render_passes(M, (long)cand_off);
+  b->passes = render_passes(M, (long)cand_off, (long)ray_off, ctx->n_cu);
   b->ev.resize((size_t)std::max(1, b->loop_iters) * b->groups.size() * ev_per_iter(b) + 2);
   b->join_ev.resize(b->groups.size());
   for (auto& e : b->ev)
