@@ -118,10 +118,33 @@ def cpu_baseline(seconds_budget=30.0, n_pts=2048):
     except Exception:
         cores = os.cpu_count()
     threads = int(os.environ.get("OMP_NUM_THREADS", cores))
-    return {"value": 1.0 / per_obj, "unit": "object-reconstructions/sec", "cores": min(threads, cores),
-            "kind": "port",
-            "sample": f"oracle/dsr_oracle.py (numpy fp32) on 1 KITTI object x {n_pts} pts, {done} of "
-                      f"{P.num_iterations} GN iterations timed ({dt:.1f} s), extrapolated to 10"}
+    out = {"value": 1.0 / per_obj, "unit": "object-reconstructions/sec", "cores": min(threads, cores),
+           "kind": "port",
+           "sample": f"oracle/dsr_oracle.py (numpy fp32) on 1 KITTI object x {n_pts} pts, {done} of "
+                     f"{P.num_iterations} GN iterations timed ({dt:.1f} s), extrapolated to 10"}
+    out.update(reference_calibration(out["value"]))
+    return out
+
+
+def reference_calibration(port_value):
+    """The port's speed relative to the reference's own CPU path, measured side by side in the
+    build container (tools/cpu_calibrate.py -> profiles/r4_cpu_calibration.json: golden F4 kitti0,
+    same thread counts, median of 3): reference-equivalent = port value / (port / reference).
+    The box's host differs from that container; the ratio at the container's full thread count
+    is the one applied."""
+    path = os.path.join(REPO, "profiles", "r4_cpu_calibration.json")
+    try:
+        cal = json.load(open(path))
+    except Exception:
+        return {}
+    th = cal["host"]["nproc"]
+    ratio = cal["runs"].get(f"port_to_reference_ratio_{th}t")
+    if not ratio:
+        return {}
+    return {"port_to_reference_ratio": round(ratio, 4), "reference_equivalent_value": port_value / ratio,
+            "calibration": f"{os.path.relpath(path, REPO)}: port {cal['runs'][f'oracle_{th}t']['obj_per_s']:.4f} vs "
+                           f"reference {cal['runs'][f'reference_{th}t']['obj_per_s']:.4f} obj/s at {th} threads "
+                           f"(1 thread: ratio {cal['runs'].get('port_to_reference_ratio_1t', float('nan')):.3f})"}
 
 
 def pmc_traffic(kernel):
@@ -149,7 +172,9 @@ def stats_sum(acc, st):
             acc[k] = max(acc.get(k, 0.0), v)
         elif k in ("lite_min_margin",):
             acc[k] = min(acc.get(k, 1e30), v)
-        elif k in ("lite", "keep_masks", "surface_in_exact", "test_hooks"):
+        elif k in ("lite", "keep_masks", "surface_in_exact", "test_hooks", "lite_eligible", "audit",
+                   "audit_shell", "audit_log2", "lite_margin0", "lite_floor", "lite_safety", "graph_captures",
+                   "graph_replays"):
             acc[k] = v
         else:
             acc[k] = acc.get(k, 0) + v
@@ -218,17 +243,19 @@ def measured_mfma_loop(device=0, ms=300.0):
     return out
 
 
-def keyframe_leg(dec, n_keyframes=6, objects=4):
+def keyframe_leg(dec, n_keyframes=12, objects=4):
     """BASELINE config 5: Redwood parameters, per keyframe `objects` new detections, each
     also run as its flipped hypothesis (LocalMapping_util.cc:394-410), 512 points, 5 GN
     iterations — one batched asynchronous call per keyframe
     (Optimizer.reconstruct_keyframe_async), so the host is free for the reference's
     LocalBundleAdjustment (LocalMapping.cc:99-128) while the GPU works.  Reports ms per
-    keyframe (uploads included) and the host time spent while batches were in flight."""
+    keyframe (uploads and download included) and the host time spent while batches were in
+    flight, for each keyframe mode: "graph" (the default: one fixed-capacity slot batch refilled
+    per keyframe, every run a replay of ONE captured hipGraph), "slot" (the same slot run
+    eagerly) and "oneshot" (a new batch per keyframe)."""
     from reconstruct.optimizer import Optimizer
     from reconstruct.utils import ForceKeyErrorDict
 
-    opt = Optimizer(dec, ForceKeyErrorDict(data_type="Redwood", optimizer=S.REDWOOD_OPTIM))
     kfs = []
     for k in range(n_keyframes):
         dets = []
@@ -236,24 +263,38 @@ def keyframe_leg(dec, n_keyframes=6, objects=4):
             o = S.redwood_object(100 * k + i)
             dets.append((o.t_cam_obj, o.pts, o.rays, o.depth, None, False))
         kfs.append(dets)
-    opt.reconstruct_keyframe(kfs[0])                  # warm-up
-    t0 = time.perf_counter()
-    host_s = 0.0
-    good = 0
-    for dets in kfs:
-        h = opt.reconstruct_keyframe_async(dets)
-        t1 = time.perf_counter()
-        while not h.done():                           # stand-in for host-side BA
-            pass
-        host_s += time.perf_counter() - t1
-        good += sum(r["is_good"] for r in h.wait())
-    dt = time.perf_counter() - t0
-    return {"keyframes": n_keyframes, "detections_per_keyframe": objects,
-            "objects_per_keyframe_batch": 2 * objects,
-            "ms_per_keyframe": round(dt / n_keyframes * 1e3, 3), "good_detections": good,
-            "host_free_ms_per_keyframe": round(host_s / n_keyframes * 1e3, 3),
-            "note": "Redwood params, 512 pts, 712 rays, 5 iters; original + flipped hypothesis per "
-                    "detection in one async batch (includes H2D upload and result download)"}
+    modes = {}
+    for mode in ("oneshot", "slot", "graph"):
+        opt = Optimizer(dec, ForceKeyErrorDict(data_type="Redwood", optimizer=S.REDWOOD_OPTIM))
+        opt.keyframe_mode = mode
+        opt.reconstruct_keyframe(kfs[0])              # warm-up (and, for "graph", the capture)
+        t0 = time.perf_counter()
+        host_s = 0.0
+        good = 0
+        for dets in kfs:
+            h = opt.reconstruct_keyframe_async(dets)
+            t1 = time.perf_counter()
+            while not h.done():                       # stand-in for host-side BA
+                pass
+            host_s += time.perf_counter() - t1
+            good += sum(r["is_good"] for r in h.wait())
+        dt = time.perf_counter() - t0
+        modes[mode] = {"ms_per_keyframe": round(dt / n_keyframes * 1e3, 3),
+                       "host_free_ms_per_keyframe": round(host_s / n_keyframes * 1e3, 3), "good_detections": good}
+        if mode != "oneshot":
+            from reconstruct import _libdsr as L
+
+            st = L.Stats()
+            opt._ctx.check(opt._ctx.lib.dsr_batch_stats(opt._slots[0].handle, C.byref(st)), "stats")
+            modes[mode].update(slot_batches=len(opt._slots), graph_captures=st.graph_captures,
+                               graph_replays=st.graph_replays)
+        opt.close_slots()
+    out = {"keyframes": n_keyframes, "detections_per_keyframe": objects, "objects_per_keyframe_batch": 2 * objects,
+           "mode": "graph", "modes": modes,
+           "note": "Redwood params, 512 pts, 712 rays, 5 iters; original + flipped hypothesis per detection in one "
+                   "async batch (includes H2D upload and result download)"}
+    out.update(modes["graph"])
+    return out
 
 
 def spawn_ranks(n):
@@ -289,7 +330,15 @@ def fp32_algorithmic(a, steps, elapsed, stats_steps=None):
                     "with one fp16 product (DESIGN.md §3.3-3.4)"}
 
 
-def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_pts=4096):
+def record_rows(res):
+    """Gathered out-records as float32 rows (loss, is_good, iters, T[16], code[64]) — what
+    --dump-records writes, for bitwise comparisons across rank counts."""
+    return np.array([[r["loss"], float(r["is_good"]), r["iters_done"]]
+                     + (list(np.asarray(r["t_cam_obj"]).reshape(-1)) + list(r["code"])
+                        if r["is_good"] else [np.nan] * 80) for r in res], np.float32)
+
+
+def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_pts=4096, dump=""):
     """BASELINE config 4: ONE job of 64 synthetic KITTI objects x 4096 points, LPT-sharded over
     the ranks (8 per GPU at N=8) with the record gather; same timing rules as the main line."""
     from reconstruct.parallel import ResidentShard
@@ -304,12 +353,15 @@ def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_
         barrier()
         t0 = time.perf_counter()
         good = 0
+        res = None
         for _ in range(steps):
             res = shard.run()
             if res is not None:
                 good += sum(int(r["is_good"]) for r in res)
         barrier()
         el = time.perf_counter() - t0
+        if dump and res is not None:
+            np.save(dump, record_rows(res))
         if dist is not None:
             t = torch.tensor([el], dtype=torch.float64, device=coll_dev or "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -317,7 +369,7 @@ def config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=3, n_obj=64, n_
         return {"value": n_obj * steps / el, "unit": "object-reconstructions/sec", "steps": steps,
                 "ms_per_step": el / steps * 1e3, "objects": n_obj, "pts": n_pts, "rays": n_pts + 200,
                 "shard_objects": [len(s) for s in shard.shards], "good_fraction": good / float(n_obj * steps),
-                "note": "BASELINE configs[3]: 64 x 4096-point objects, one job LPT-sharded over the ranks"}
+                "note": f"BASELINE configs[3]: {n_obj} x {n_pts}-point objects, one job LPT-sharded over the ranks"}
     finally:
         shard.close()
 
@@ -355,7 +407,9 @@ def small_legs(opt, objs, steps=3):
                                        "Optimizer.reconstruct_object call (H2D + run + D2H)"}}
 
 
-def main():
+def parse_args():
+    """Arguments and world size.  ``--gpus N`` (N > 1) without a launcher: spawn the ranks and
+    exit with their status; under a launcher without ``--gpus``: the launcher's rank count."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -366,14 +420,25 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the exact-decode and keyframe legs")
     ap.add_argument("--no-config4", action="store_true", help="skip the 64 x 4096-point config-4 leg")
-    ap.add_argument("--dump-records", default="", help="rank 0 writes the last step's gathered records (.npy)")
+    ap.add_argument("--dump-records", default="", help="rank 0 writes the last step's gathered records (.npy; "
+                                                       "the config-4 leg's to <name>_c4.npy)")
+    ap.add_argument("--c4-objects", type=int, default=64, help="config-4 leg: objects (rehearsals only)")
+    ap.add_argument("--c4-pts", type=int, default=4096, help="config-4 leg: points per object (rehearsals only)")
+    gpus_given = any(a == "--gpus" or a.startswith("--gpus=") for a in sys.argv[1:])
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if not gpus_given:                       # under a launcher without --gpus: its ranks
+        args.gpus = world
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    return args, world
+
+
+def main():
+    args, world = parse_args()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -461,9 +526,7 @@ def main():
         ranks.update(backend=dist.get_backend(), world_size_observed=dist.get_world_size(),
                      rank_seconds=[round(x, 4) for x in per_rank])
     if args.dump_records and rank == 0 and res is not None:
-        np.save(args.dump_records, np.array([[r["loss"], float(r["is_good"]), r["iters_done"]]
-                                             + (list(np.asarray(r["t_cam_obj"]).reshape(-1)) + list(r["code"])
-                                                if r["is_good"] else [np.nan] * 80) for r in res], np.float32))
+        np.save(args.dump_records, record_rows(res))
     value = n_job * args.steps / elapsed
     roof = kernel_rooflines(acc) if acc else {}
     loop = measured_mfma_loop(local) if rank == 0 and acc and not args.no_extra else None
@@ -521,6 +584,15 @@ def main():
             "fp32_algorithmic": fp32_algorithmic(acc, args.steps, elapsed, stats_steps) if acc else None,
             "lite_broken_blocks": acc.get("lite_broken_blocks"),
             "test_hooks": acc.get("test_hooks"),
+            # the lite pass's guard as the timed batches ran it (dsr_stats, ABI 8) and the decoder's
+            # load-time qualification (dsr_decoder_info): not switchable without DSR_TEST_HOOKS=1
+            "lite_guard": {"decoder_lite_eligible": bool(acc.get("lite_eligible")), "audit": acc.get("audit"),
+                           "audit_shell_margins": acc.get("audit_shell"), "audit_hashed_share_log2": acc.get("audit_log2"),
+                           "margin_first_iteration": acc.get("lite_margin0"), "margin_floor": acc.get("lite_floor"),
+                           "margin_safety": acc.get("lite_safety"),
+                           "decoder_probe": {k: dec.info[k] for k in ("lite_probe_ratio", "lite_probe_max_err",
+                                                                     "lite_probe_max_err_all", "probe_points",
+                                                                     "probe_codes", "probe_ms")}},
             "ranks": ranks,
             # device wall of one run (HIP events around dsr_batch_run's work, rank 0): the rest of
             # ms_per_step is host time (launch, download, packing, stats)
@@ -548,7 +620,9 @@ def main():
         out["batch_create_ms"] = create_warm_s * 1e3
         out["host_inclusive_value"] = n_job / (elapsed / args.steps + create_warm_s)
     if not args.no_config4 and not args.weak:
-        c4 = config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=min(args.steps, 3))
+        c4 = config4_leg(opt, rank, coll_dev, barrier, dist, torch, steps=min(args.steps, 3), n_obj=args.c4_objects,
+                         n_pts=args.c4_pts,
+                         dump=args.dump_records[:-4] + "_c4.npy" if args.dump_records.endswith(".npy") else "")
         if rank == 0:
             out["config4"] = c4
     if world == 1 and not args.no_extra:

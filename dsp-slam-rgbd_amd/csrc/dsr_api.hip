@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -44,6 +45,10 @@ struct dsr_ctx {
   // guards pool / ev_*: a context is used from one thread at a time (include/dsr.h), but
   // batches of async handles may be destroyed from another Python thread (finalizers)
   std::mutex mu;
+  // serialises the stream work of batch entry points (launch, graph capture, refill, redo) with
+  // dsr_batch_destroy: a destroy from a finalizer thread synchronises the context's streams and
+  // destroys a graph, which must never happen while the owning thread captures on that stream
+  std::recursive_mutex run_mu;
 };
 static constexpr size_t POOL_CAP = (size_t)16 << 30;
 
@@ -167,6 +172,7 @@ struct dsr_decoder {
   size_t bytes = 0;
   DevDecoder D{};
   int code_len = 64;
+  dsr_decoder_info info{};      // load-time lite qualification (decoder_qualify)
 };
 
 struct DevBuf {
@@ -240,6 +246,22 @@ struct dsr_batch {
   bool timed = false;               // last run recorded per-kernel events (eager run)
   hipGraphExec_t graph = nullptr;   // the whole run, captured on the 2nd dsr_batch_run
   long graph_key = -1;              // kernel variants the graph was captured with
+  int captures = 0, replays = 0;    // graph captures / replays over the batch's life
+  // Fixed-capacity batches (dsr_batch_create_capacity): n_obj slots of max_pts / max_rays each;
+  // dsr_batch_refill uploads a new object set into them (pinned staging, one stream-ordered
+  // copy per input buffer) and rewrites the per-slot descriptors, so every kernel argument —
+  // and a captured graph — stays valid from one keyframe to the next.
+  bool capacity = false;
+  bool cap_graph = false;           // DSR_BATCH_GRAPH: every run replays one captured graph
+  int max_pts = 0, max_rays = 0;
+  int n_active = 0;                 // objects of the current fill (out-records downloaded)
+  struct Stage {                    // pinned host mirrors of the refilled input buffers
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t bytes = 0;
+  };
+  std::vector<Stage> stage;
+  hipEvent_t up_ev = nullptr;       // recorded after the last refill's uploads
 };
 
 #define DSR_CHECK(ctx, call)                                                        \
@@ -353,6 +375,8 @@ static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
         }
   return sw;
 }
+
+static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec);
 
 int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, size_t n_floats,
                      dsr_decoder** out) {
@@ -530,6 +554,12 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
     D.Wbh_raw[l] = reinterpret_cast<const _Float16*>(P(hb16[l]));
     D.swb[l] = swb16[l];
   }
+  const int rc = decoder_qualify(ctx, dec);       // may a batch trust the lite pass with it?
+  if (rc) {
+    hipFree(dec->dmem);
+    delete dec;
+    return rc;
+  }
   *out = dec;
   return 0;
 }
@@ -619,46 +649,54 @@ static hipError_t pool_event(dsr_ctx* ctx, hipEvent_t* e, bool timing) {
   return timing ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
 }
 
-// Lite-pass audit (dsr_dev.hpp: lite_flag).  DSR_LITE_AUDIT=0 disables it; DSR_LITE_SHELL
-// (1.0): out-of-band samples with |y| < th + (1 + shell)*margin — `shell` margins beyond the
-// band edge — are audited; DSR_LITE_AUDIT_LOG2 (7): plus a hashed 2^-log2 share of all other
-// decoded samples (0: all of them — the audit-everything survey, tools/lite_audit_all.py);
-// DSR_LITE_PERTURB: test hook
+// Lite-pass audit (dsr_dev.hpp: lite_flag): the shipped guard is always on — out-of-band
+// samples with |y| < th + (1 + shell)*margin, shell = 1 (`shell` margins beyond the band edge),
+// are audited, plus a hashed 2^-7 share of all other decoded samples.  Only under
+// DSR_TEST_HOOKS=1 (reported in dsr_stats.test_hooks) does a batch read DSR_LITE_AUDIT (0: off),
+// DSR_LITE_SHELL, DSR_LITE_AUDIT_LOG2 (0: every sample — the audit-everything survey,
+// tools/lite_audit_all.py) and the DSR_LITE_PERTURB test hook: a stray variable cannot switch
+// off or thin out the misclassification guard of a production run.
+static float env_hook(bool hooks, const char* k, float d) {
+  const char* e = hooks ? getenv(k) : nullptr;
+  return e ? (float)atof(e) : d;
+}
 static ErtArgs lite_settings(bool hooks) {
-  auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
   ErtArgs E{};
-  const char* a = getenv("DSR_LITE_AUDIT");
-  E.audit = (a && atoi(a) == 0) ? 0 : 1;
-  E.shell = envf("DSR_LITE_SHELL", 1.0f);
-  E.audit_log2 = std::max(0, std::min(24, (int)envf("DSR_LITE_AUDIT_LOG2", 7.0f)));
-  E.perturb = hooks ? envf("DSR_LITE_PERTURB", 0.0f) : 0.0f;
+  E.audit = env_hook(hooks, "DSR_LITE_AUDIT", 1.0f) == 0.0f ? 0 : 1;
+  E.shell = env_hook(hooks, "DSR_LITE_SHELL", 1.0f);
+  E.audit_log2 = std::max(0, std::min(24, (int)env_hook(hooks, "DSR_LITE_AUDIT_LOG2", 7.0f)));
+  E.perturb = env_hook(hooks, "DSR_LITE_PERTURB", 0.0f);
   E.lag = lite_lag(hooks);
   return E;
 }
 
-static GNParams make_params(const dsr_optim_params* p) {
+static GNParams make_params(const dsr_optim_params* p, bool hooks) {
   GNParams P;
   P.k1 = p->k1; P.k2 = p->k2; P.k3 = p->k3; P.k4 = p->k4;
   P.b1 = p->b1; P.b2 = p->b2; P.lr = p->lr; P.s_damp = p->s_damp;
   P.cut_off = p->cut_off; P.iters = p->num_iterations; P.M = p->num_depth_samples;
   P.raw_residual = 0;
-  auto envf = [](const char* k, float d) { const char* e = getenv(k); return e ? (float)atof(e) : d; };
   // lite-pass margin: th in the first iteration, then max(0.002, 4 x the
-  // largest |lite - exact| the object's band and audit samples showed; the audit guards it)
-  P.lite_margin0 = envf("DSR_LITE_MARGIN", p->cut_off);     // th (0.01 in every reference config)
-  P.lite_floor = envf("DSR_LITE_FLOOR", 0.002f);
-  P.lite_safety = envf("DSR_LITE_SAFETY", 4.0f);
+  // largest |lite - exact| the object's band and audit samples showed; the audit guards it).
+  // DSR_LITE_MARGIN / _FLOOR / _SAFETY only under DSR_TEST_HOOKS=1 (lite_settings)
+  P.lite_margin0 = env_hook(hooks, "DSR_LITE_MARGIN", p->cut_off);   // th (0.01 in every reference config)
+  P.lite_floor = env_hook(hooks, "DSR_LITE_FLOOR", 0.002f);
+  P.lite_safety = env_hook(hooks, "DSR_LITE_SAFETY", 4.0f);
   return P;
 }
 
 int dsr_batch_destroy(dsr_batch* b) {
   if (!b) return 0;
   dsr_ctx* ctx = b->ctx;
+  std::lock_guard<std::recursive_mutex> run(ctx->run_mu);
   hipSetDevice(ctx->device);
   // the blocks go back to the pool: no kernel of this batch may still be using them
   for (size_t g = 0; g < std::max<size_t>(1, b->groups.size()); ++g) hipStreamSynchronize(ctx->gstream[g]);
   if (b->graph) hipGraphExecDestroy(b->graph);
+  for (auto& sg : b->stage)
+    if (sg.host) hipHostFree(sg.host);
   std::lock_guard<std::mutex> lk(ctx->mu);
+  if (b->up_ev) ctx->ev_plain.push_back(b->up_ev);
   for (auto& e : b->ev)
     if (e) ctx->ev_timing.push_back(e);
   for (hipEvent_t e : b->join_ev)
@@ -680,7 +718,8 @@ int dsr_batch_destroy(dsr_batch* b) {
 static bool graph_enabled();
 
 static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p,
-                             int n_obj, const dsr_object_in* in, bool trace, dsr_batch** out) {
+                             int n_obj, const dsr_object_in* in, bool trace, dsr_batch** out,
+                             bool one_group = false) {
   if (!ctx || !dec || !p || !out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
   *out = nullptr;
   if (n_obj <= 0) return fail(ctx, "n_obj must be > 0");
@@ -692,8 +731,10 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   auto* b = new dsr_batch();
   b->ctx = ctx;
   b->dec = dec;
-  b->P = make_params(p);
+  b->hooks = test_hooks();
+  b->P = make_params(p, b->hooks);
   b->n_obj = n_obj;
+  b->n_active = n_obj;
   b->iters = p->num_iterations;
   b->M = p->num_depth_samples;
   const int M = b->M;
@@ -750,7 +791,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     // one-group graph replays 3% faster than a one-group eager run (5.31 vs 5.46 ms; r3k,
     // tools/graph_queues.py).  Results are bitwise the same for any grouping.
     const char* e = getenv("DSR_STREAMS");
-    int G = e ? atoi(e) : graph_enabled() ? 1 : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
+    int G = e ? atoi(e) : (graph_enabled() || one_group) ? 1 : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
     G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
     if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
     for (int g = 0; g < G; ++g) {
@@ -782,8 +823,10 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
   {
+    // the lite pass runs only on decoders that passed their load-time qualification
+    // (decoder_qualify); DSR_LITE=0 decodes every sample exactly on any decoder
     const char* e = getenv("DSR_LITE");
-    b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1);
+    b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1) && dec->info.lite_eligible;
   }
   if (b->lite) {
     const char* km = getenv("DSR_KEEP_MASKS");
@@ -845,7 +888,6 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
   ALLOC(b->sred, sizeof(float) * 2 * SLOT_FLOATS * (size_t)n_obj);
-  b->hooks = test_hooks();
   b->lite_cfg = lite_settings(b->hooks);
   b->loop_iters = b->iters + ((b->lite && b->lite_cfg.audit && b->iters > 0) ? 1 : 0);
   ALLOC(b->diag, sizeof(int) * STD_INTS);
@@ -896,6 +938,121 @@ int dsr_batch_create(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_param
   return batch_create_impl(ctx, dec, p, n_obj, in, false, out);
 }
 
+// A capacity batch is an ordinary batch laid out for max_obj objects of max_pts points and
+// max_rays rays each (every buffer, tile table, render-chunk table and object group sized for
+// that), whose slots dsr_batch_refill fills; slots without an object hold an empty object (no
+// points, no rays: the reference's numeric failure, which every kernel skips after iteration 0).
+int dsr_batch_create_capacity(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int max_obj,
+                              int max_pts, int max_rays, int flags, dsr_batch** out) {
+  if (!ctx || !dec || !p || !out) return fail(ctx, "null argument");
+  *out = nullptr;
+  if (max_obj <= 0 || max_pts < 0 || max_rays < 0) return fail(ctx, "capacities must be > 0");
+  if (flags & ~DSR_BATCH_GRAPH) return fail(ctx, "unknown batch flags");
+  const std::vector<float> zp((size_t)std::max(1, max_pts) * 3, 0.f), zr((size_t)std::max(1, max_rays) * 3, 0.f);
+  std::vector<dsr_object_in> in(max_obj);
+  for (auto& x : in) {
+    x = dsr_object_in{};
+    for (int i = 0; i < 16; i += 5) x.t_cam_obj[i] = 1.f;
+    x.pts = zp.data();
+    x.n_pts = max_pts;
+    x.rays = zr.data();
+    x.n_rays = max_rays;
+    x.depth = nullptr;
+    x.n_depth = 0;
+  }
+  dsr_batch* b = nullptr;
+  int rc = batch_create_impl(ctx, dec, p, max_obj, in.data(), false, &b, (flags & DSR_BATCH_GRAPH) != 0);
+  if (rc) return rc;
+  b->capacity = true;
+  b->cap_graph = (flags & DSR_BATCH_GRAPH) != 0;
+  b->max_pts = max_pts;
+  b->max_rays = max_rays;
+  const std::pair<void*, size_t> bufs[] = {
+      {b->desc, sizeof(ObjDesc) * max_obj},          {b->t_in, sizeof(float) * 16 * max_obj},
+      {b->z_in, sizeof(float) * CODE * max_obj},     {b->is_oc, sizeof(int) * max_obj},
+      {b->pts, sizeof(float) * 3 * (size_t)max_obj * max_pts},
+      {b->rays, sizeof(float) * 3 * (size_t)max_obj * max_rays},
+      {b->dobs, sizeof(float) * (size_t)max_obj * max_rays}};
+  for (const auto& kv : bufs) {
+    dsr_batch::Stage sg;
+    sg.dev = kv.first;
+    sg.bytes = std::max<size_t>(kv.second, 4);
+    if (hipHostMalloc(&sg.host, sg.bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      dsr_batch_destroy(b);
+      return fail(ctx, "hipHostMalloc failed (capacity batch staging)");
+    }
+    std::memset(sg.host, 0, sg.bytes);
+    b->stage.push_back(sg);
+  }
+  if (pool_event(ctx, &b->up_ev, false) != hipSuccess) {
+    dsr_batch_destroy(b);
+    return fail(ctx, "hipEventCreate failed");
+  }
+  rc = dsr_batch_refill(b, 0, nullptr);          // every slot empty until the first fill
+  if (rc) {
+    dsr_batch_destroy(b);
+    return rc;
+  }
+  *out = b;
+  return 0;
+}
+
+int dsr_batch_refill(dsr_batch* b, int n_obj, const dsr_object_in* in) {
+  if (!b) return -2;
+  dsr_ctx* ctx = b->ctx;
+  if (!b->capacity) return fail(ctx, "dsr_batch_refill needs a batch from dsr_batch_create_capacity");
+  if (n_obj < 0 || n_obj > b->n_obj || (n_obj > 0 && !in))
+    return fail(ctx, "refill: n_obj must be in [0, the batch's object capacity]");
+  for (int o = 0; o < n_obj; ++o) {
+    const dsr_object_in& x = in[o];
+    if (x.n_pts < 0 || x.n_pts > b->max_pts || (x.n_pts > 0 && !x.pts))
+      return fail(ctx, "refill: surface points exceed the batch capacity (or are null)");
+    if (x.n_rays < 0 || x.n_rays > b->max_rays || (x.n_rays > 0 && !x.rays))
+      return fail(ctx, "refill: rays exceed the batch capacity (or are null)");
+    if (x.n_depth < 0 || x.n_depth > x.n_rays || (x.n_depth > 0 && !x.depth))
+      return fail(ctx, "depth must hold at most n_rays foreground values");
+  }
+  std::lock_guard<std::recursive_mutex> run(ctx->run_mu);
+  hipSetDevice(ctx->device);
+  // the previous refill's copies read the staging buffers until they complete
+  DSR_CHECK(ctx, hipEventSynchronize(b->up_ev));
+  auto* desc = static_cast<ObjDesc*>(b->stage[0].host);
+  auto* t_in = static_cast<float*>(b->stage[1].host);
+  auto* z_in = static_cast<float*>(b->stage[2].host);
+  auto* is_oc = static_cast<int*>(b->stage[3].host);
+  auto* pts = static_cast<float*>(b->stage[4].host);
+  auto* rays = static_cast<float*>(b->stage[5].host);
+  auto* dobs = static_cast<float*>(b->stage[6].host);
+  for (int o = 0; o < b->n_obj; ++o) {
+    ObjDesc d = b->hdesc[o];                       // the slot's offsets; the fill's counts
+    const dsr_object_in* x = o < n_obj ? &in[o] : nullptr;
+    d.n_pts = x ? x->n_pts : 0;
+    d.n_rays = x ? x->n_rays : 0;
+    d.n_fg = x ? x->n_depth : 0;
+    desc[o] = d;
+    float* t = t_in + (size_t)o * 16;
+    for (int i = 0; i < 16; ++i) t[i] = x ? x->t_cam_obj[i] : (i % 5 == 0 ? 1.f : 0.f);
+    float* z = z_in + (size_t)o * CODE;
+    if (x && x->code) std::memcpy(z, x->code, sizeof(float) * CODE);
+    else std::memset(z, 0, sizeof(float) * CODE);
+    is_oc[o] = (x && x->pose_is_obj_cam) ? 1 : 0;
+    if (!x) continue;
+    if (x->n_pts) std::memcpy(pts + (size_t)d.pts_off * 3, x->pts, sizeof(float) * 3 * x->n_pts);
+    if (x->n_rays) std::memcpy(rays + (size_t)d.ray_off * 3, x->rays, sizeof(float) * 3 * x->n_rays);
+    for (int r = 0; r < x->n_rays; ++r) dobs[d.ray_off + r] = r < x->n_depth ? x->depth[r] : 0.f;
+  }
+  hipStream_t s = ctx->stream;                     // ordered after the previous run's work
+  for (const auto& sg : b->stage)
+    DSR_CHECK(ctx, hipMemcpyAsync(sg.dev, sg.host, sg.bytes, hipMemcpyHostToDevice, s));
+  // lite flags of the previous fill's rays beyond the new counts are never read, but start clean
+  if (b->refine) DSR_CHECK(ctx, hipMemsetAsync(b->refine, 0, (size_t)std::max(1, b->cand_total), s));
+  DSR_CHECK(ctx, hipEventRecord(b->up_ev, s));
+  b->n_active = n_obj;
+  b->ran = false;
+  return 0;
+}
+
 static int batch_enqueue(dsr_batch* b, bool timing = true);
 static int batch_finish(dsr_batch* b);
 
@@ -936,20 +1093,26 @@ static int batch_capture(dsr_batch* b) {
   hipGraphDestroy(g);
   DSR_CHECK(ctx, ei);
   b->graph_key = graph_key();
+  ++b->captures;
   return 0;
 }
 
 int dsr_batch_graph(dsr_batch* b) {
   if (!b) return -2;
+  std::lock_guard<std::recursive_mutex> run(b->ctx->run_mu);
   hipSetDevice(b->ctx->device);
-  if (!graph_enabled()) return 0;
+  if (!graph_enabled() && !b->cap_graph) return 0;
   b->runs = std::max(b->runs, 1);
   return batch_capture(b);
 }
 
 static int batch_launch(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
-  if (!graph_enabled() || b->runs++ == 0) {
+  if (b->capacity && b->n_active == 0) return fail(ctx, "capacity batch holds no objects (dsr_batch_refill)");
+  // a DSR_BATCH_GRAPH capacity batch replays from its first run (its refills keep every kernel
+  // argument); other batches under DSR_GRAPH=1 run eagerly once, then replay
+  const bool first_eager = !b->cap_graph;
+  if (!(graph_enabled() || b->cap_graph) || (b->runs++ == 0 && first_eager)) {
     const int rc = batch_enqueue(b);
     if (rc) return rc;
     b->ran = true;
@@ -967,6 +1130,7 @@ static int batch_launch(dsr_batch* b) {
   DSR_CHECK(ctx, hipMemsetAsync(b->out, 0xff, sizeof(dsr_object_out) * b->n_obj, ctx->stream));
   DSR_CHECK(ctx, hipGraphLaunch(b->graph, ctx->stream));
   DSR_CHECK(ctx, hipEventRecord(b->ev[1], ctx->stream));
+  ++b->replays;
   b->spare_run = false;          // a replay runs the regular iterations only (batch_finish)
   b->ran = true;
   b->timed = false;
@@ -976,6 +1140,7 @@ static int batch_launch(dsr_batch* b) {
 int dsr_batch_run(dsr_batch* b) {
   if (!b) return -2;
   dsr_ctx* ctx = b->ctx;
+  std::lock_guard<std::recursive_mutex> run(ctx->run_mu);
   hipSetDevice(ctx->device);
   const int rc = batch_launch(b);
   if (rc) return rc;
@@ -988,6 +1153,7 @@ static int batch_redo(dsr_batch* b);
 int dsr_batch_query(dsr_batch* b) {
   if (!b) return -2;
   if (!b->ran) return fail(b->ctx, "batch has not run");
+  std::lock_guard<std::recursive_mutex> run(b->ctx->run_mu);
   hipSetDevice(b->ctx->device);
   const hipError_t e = hipEventQuery(b->done_ev);
   if (e == hipSuccess) {
@@ -1034,6 +1200,7 @@ static int batch_redo(dsr_batch* b) {
 }
 static int batch_finish(dsr_batch* b) {
   dsr_ctx* ctx = b->ctx;
+  std::lock_guard<std::recursive_mutex> run(ctx->run_mu);
   DSR_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   const int rc = batch_redo(b);
   if (rc < 0) return rc;
@@ -1163,7 +1330,7 @@ int dsr_batch_download(dsr_batch* b, dsr_object_out* out) {
     const int rc = batch_finish(b);
     if (rc) return rc;
   }
-  DSR_CHECK(b->ctx, hipMemcpyAsync(out, b->out, sizeof(dsr_object_out) * b->n_obj, hipMemcpyDeviceToHost,
+  DSR_CHECK(b->ctx, hipMemcpyAsync(out, b->out, sizeof(dsr_object_out) * b->n_active, hipMemcpyDeviceToHost,
                                    b->ctx->stream));
   DSR_CHECK(b->ctx, hipStreamSynchronize(b->ctx->stream));
   return 0;
@@ -1177,7 +1344,7 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
     const int rc = batch_finish(b);
     if (rc) return rc;
   }
-  std::memset(st, 0, sizeof(*st));
+  *st = dsr_stats{};
   float ms = 0.f;
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
@@ -1208,6 +1375,15 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->refine_launches = (b->timed && b->lite) ? used_iters * G : 0;
   st->lite = b->lite ? 1 : 0;
   st->test_hooks = b->hooks ? 1 : 0;
+  st->lite_eligible = b->dec->info.lite_eligible;
+  st->audit = (b->lite && b->lite_cfg.audit) ? 1 : 0;
+  st->audit_shell = b->lite_cfg.shell;
+  st->audit_log2 = b->lite_cfg.audit_log2;
+  st->lite_margin0 = b->P.lite_margin0;
+  st->lite_floor = b->P.lite_floor;
+  st->lite_safety = b->P.lite_safety;
+  st->graph_captures = b->captures;
+  st->graph_replays = b->replays;
   {
     int nb = 0;
     DSR_CHECK(b->ctx, hipMemcpy(&nb, b->diag + STD_BROKEN, sizeof(int), hipMemcpyDeviceToHost));
@@ -1355,6 +1531,155 @@ __global__ void k_fold_code(DevDecoder D, const float* __restrict__ z, float* __
   }
   bias0f[n] = D.bias[0][n] + s0;
   bias4f[n] = D.bias[4][n] + s4;
+}
+
+// ------------------------------------------------------------------------------------
+// load-time qualification of the lite pass (include/dsr.h: dsr_decoder_info)
+// ------------------------------------------------------------------------------------
+// The lite pass classifies ray samples with one fp16 product; the per-object margin and the
+// audit guard it at run time, but their evidence is empirical: a decoder with
+// larger weights or activations has larger fp16 errors.  So before any batch trusts the lite
+// pass with a loaded decoder, the decoder decodes a fixed probe set through both passes — the
+// same kernels, tiles and bias fold a batch uses — and the lite error is measured against the
+// distance of each exact value to its nearest class boundary (full <= -th < band < th <=
+// empty, th = 0.01, loss_utils.py:40-48, loss.py:98-102), floored at the margin floor 0.002, and
+// against the floor itself near the surface (|exact| < 0.1, where the band and the audit shell
+// lie).  Above half of either anywhere, the decoder is lite-ineligible and every batch decodes
+// exactly.
+static constexpr int PROBE_POINTS = 65536, PROBE_CODES = 4;
+static constexpr float PROBE_TH = 0.01f, PROBE_FLOOR = 0.002f, PROBE_MAX_RATIO = 0.5f;
+
+static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int n = PROBE_POINTS, nc = PROBE_CODES, tot = n * nc;
+  uint64_t s = 0x9E3779B97F4A7C15ull;           // fixed LCG: the probe set is part of the contract
+  auto u01 = [&]() {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)(s >> 11) * (1.0 / 9007199254740992.0);
+  };
+  std::vector<float4> cand(tot);
+  for (int i = 0; i < n;) {                     // uniform in the unit ball (rejection from the cube)
+    const double x = 2 * u01() - 1, y = 2 * u01() - 1, z = 2 * u01() - 1;
+    if (x * x + y * y + z * z >= 1.0) continue;
+    for (int c = 0; c < nc; ++c) {
+      int idx = i;
+      float fi;
+      std::memcpy(&fi, &idx, sizeof(float));
+      cand[(size_t)c * n + i] = make_float4((float)x, (float)y, (float)z, fi);
+    }
+    ++i;
+  }
+  static const float scale[PROBE_CODES] = {0.0f, 0.1f, 0.3f, 1.0f};
+  std::vector<float> hz((size_t)nc * CODE);
+  for (int c = 0; c < nc; ++c)
+    for (int k = 0; k < CODE; ++k) {               // Box-Muller
+      const double r = std::sqrt(-2.0 * std::log(1.0 - u01())), t = 2.0 * M_PI * u01();
+      hz[(size_t)c * CODE + k] = (float)(scale[c] * r * std::cos(t));
+    }
+  std::vector<ObjDesc> hd(nc);
+  std::vector<ObjState> hs(nc);
+  std::vector<Tile> tl, te;
+  for (int c = 0; c < nc; ++c) {
+    hd[c] = ObjDesc{};
+    hd[c].ray_off = c * n;
+    hd[c].n_rays = n;
+    hd[c].cand_off = c * n;
+    std::memset(&hs[c], 0, sizeof(ObjState));    // lite_margin 0: flags are not used here
+    for (int t = 0; t * LTILE < n; ++t) tl.push_back(Tile{c, 0, t * LTILE, std::min(LTILE, n - t * LTILE)});
+    for (int t = 0; t * TILE < n; ++t) te.push_back(Tile{c, 0, t * TILE, std::min(TILE, n - t * TILE)});
+  }
+  const int ntl = (int)tl.size(), nte = (int)te.size();
+  std::vector<void*> al;
+  auto A = [&](void** p, size_t bytes) {
+    if (hipMalloc(p, bytes) != hipSuccess) { (void)hipGetLastError(); return false; }
+    al.push_back(*p);
+    return true;
+  };
+  struct Free {
+    std::vector<void*>& al;
+    ~Free() { for (void* p : al) hipFree(p); }
+  } guard{al};
+  float4* dc = nullptr;
+  float *dl = nullptr, *de = nullptr, *dz = nullptr, *db0 = nullptr, *db4 = nullptr;
+  unsigned char* dref = nullptr;
+  int *ddead = nullptr, *dntl = nullptr, *dnte = nullptr;
+  ObjDesc* ddesc = nullptr;
+  ObjState* dst = nullptr;
+  Tile *dtl = nullptr, *dte = nullptr;
+  if (!A((void**)&dc, sizeof(float4) * tot) || !A((void**)&dl, sizeof(float) * tot) ||
+      !A((void**)&de, sizeof(float) * tot) || !A((void**)&dz, sizeof(float) * hz.size()) ||
+      !A((void**)&db0, sizeof(float) * HID * nc) || !A((void**)&db4, sizeof(float) * HID * nc) ||
+      !A((void**)&dref, tot) || !A((void**)&ddead, sizeof(int) * tot) || !A((void**)&dntl, sizeof(int)) ||
+      !A((void**)&dnte, sizeof(int)) || !A((void**)&ddesc, sizeof(ObjDesc) * nc) ||
+      !A((void**)&dst, sizeof(ObjState) * nc) || !A((void**)&dtl, sizeof(Tile) * ntl) ||
+      !A((void**)&dte, sizeof(Tile) * nte))
+    return fail(ctx, "hipMalloc failed (lite qualification)");
+  hipStream_t st = ctx->stream;
+  DSR_CHECK(ctx, hipMemcpyAsync(dc, cand.data(), sizeof(float4) * tot, hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dz, hz.data(), sizeof(float) * hz.size(), hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(ddesc, hd.data(), sizeof(ObjDesc) * nc, hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dst, hs.data(), sizeof(ObjState) * nc, hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dtl, tl.data(), sizeof(Tile) * ntl, hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dte, te.data(), sizeof(Tile) * nte, hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dntl, &ntl, sizeof(int), hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(dnte, &nte, sizeof(int), hipMemcpyHostToDevice, st));
+  DSR_CHECK(ctx, hipMemsetAsync(dref, 0, tot, st));
+  DSR_CHECK(ctx, hipMemsetAsync(ddead, 0, sizeof(int) * tot, st));
+  const DevDecoder& D = dec->D;
+  for (int c = 0; c < nc; ++c)
+    hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, st, D, (const float*)dz + (size_t)c * CODE,
+                       db0 + (size_t)c * HID, db4 + (size_t)c * HID);
+  ErtArgs E{};
+  E.dead = ddead;
+  E.M = 1;
+  E.nth = -PROBE_TH;
+  E.st = dst;
+  E.refine = dref;
+  E.lag = lite_lag(false);
+  E.audit = 0;
+  E.shell = 1.0f;
+  E.audit_log2 = 7;
+  E.perturb = 0.0f;
+  E.diag = nullptr;
+  hipLaunchKernelGGL(lite_kernel(), dim3(ctx->n_cu), dim3(512), 0, st, D, (const Tile*)dtl, (const int*)dntl,
+                     (const ObjDesc*)ddesc, (const float4*)dc, (const float*)db0, (const float*)db4, dl, E);
+  hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(ctx->n_cu), dim3(512), 0, st, D, (const Tile*)dte,
+                     (const int*)dnte, (const ObjDesc*)ddesc, (const float4*)dc, (const float*)db0,
+                     (const float*)db4, de, (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr},
+                     MaskArgs{nullptr, nullptr, nullptr, nullptr});
+  DSR_CHECK(ctx, hipGetLastError());
+  std::vector<float> yl(tot), ye(tot);
+  DSR_CHECK(ctx, hipMemcpyAsync(yl.data(), dl, sizeof(float) * tot, hipMemcpyDeviceToHost, st));
+  DSR_CHECK(ctx, hipMemcpyAsync(ye.data(), de, sizeof(float) * tot, hipMemcpyDeviceToHost, st));
+  DSR_CHECK(ctx, hipStreamSynchronize(st));
+  double ratio = 0.0, near = 0.0, all = 0.0;
+  for (int i = 0; i < tot; ++i) {
+    const double e = ye[i], d = std::fabs((double)yl[i] - e);
+    if (!std::isfinite(e) || !(d == d)) {          // an overflowing or NaN lite value: not eligible
+      ratio = INFINITY;
+      all = INFINITY;
+      continue;
+    }
+    all = std::max(all, d);
+    if (std::fabs(e) < 0.1) near = std::max(near, d);
+    ratio = std::max(ratio, d / std::max((double)PROBE_FLOOR, std::fabs(std::fabs(e) - (double)PROBE_TH)));
+  }
+  dsr_decoder_info& I = dec->info;
+  I.code_len = dec->code_len;
+  I.lite_probe_ratio = ratio;
+  I.lite_probe_max_err = near;
+  I.lite_probe_max_err_all = all;
+  I.lite_eligible = (ratio <= PROBE_MAX_RATIO && near <= PROBE_MAX_RATIO * PROBE_FLOOR) ? 1 : 0;
+  I.probe_points = n;
+  I.probe_codes = nc;
+  I.probe_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
+int dsr_decoder_info_get(const dsr_decoder* dec, dsr_decoder_info* info) {
+  if (!dec || !info) return -2;
+  *info = dec->info;
+  return 0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1653,7 +1978,7 @@ int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_pa
             hipMemcpy(doc, zeros.data(), sizeof(int) * n, hipMemcpyHostToDevice) == hipSuccess;
   if (!ok) { cleanup(); return fail(ctx, "hipMemcpy failed (pose_only)"); }
   const DevDecoder& D = dec->D;
-  GNParams P = make_params(p);
+  GNParams P = make_params(p, false);
   P.raw_residual = 1;
   for (int o = 0; o < n_obj; ++o)
     hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)dz + (size_t)CODE * o,

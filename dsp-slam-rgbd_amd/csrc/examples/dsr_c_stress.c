@@ -81,6 +81,9 @@ static void no_device_paths(void) {
         "batch calls on NULL accepted");
   CHECK(dsr_batch_download(NULL, NULL) < 0 && dsr_batch_stats(NULL, NULL) < 0, "batch NULL accepted");
   CHECK(dsr_mesher_destroy(NULL) == 0, "mesher_destroy(NULL)");
+  CHECK(dsr_batch_refill(NULL, 0, NULL) < 0, "refill(NULL) accepted");
+  CHECK(dsr_batch_create_capacity(NULL, NULL, NULL, 1, 1, 1, 0, NULL) < 0, "create_capacity(NULL) accepted");
+  CHECK(dsr_decoder_info_get(NULL, NULL) < 0, "decoder_info_get(NULL) accepted");
   {
     float v[8] = {0};
     int nv = 0, nf = 0;
@@ -260,6 +263,50 @@ int main(int argc, char** argv) {
               out[o].iters_done);
     }
     CHECK(dsr_batch_destroy(bt) == 0, "destroy");
+  }
+
+  /* fixed-capacity batch (keyframe stream): refilled fills, eager and as one replayed graph;
+     the same objects in reverse slot order come back reversed, bitwise */
+  if (run_section("capacity")) {
+    dsr_decoder_info di;
+    CHECK(dsr_decoder_info_get(dec, &di) == 0 && di.lite_eligible == 1 && di.probe_points == 65536,
+          "decoder info: eligible %d ratio %g", di.lite_eligible, di.lite_probe_ratio);
+    int mp = 0, mr = 0;
+    for (int o = 0; o < n_obj; ++o) {
+      mp = in[o].n_pts > mp ? in[o].n_pts : mp;
+      mr = in[o].n_rays > mr ? in[o].n_rays : mr;
+    }
+    dsr_object_in* rev = (dsr_object_in*)calloc((size_t)n_obj, sizeof(dsr_object_in));
+    for (int o = 0; o < n_obj; ++o) rev[o] = in[n_obj - 1 - o];
+    /* (the graph-captured variant counts as part of the "graph" section: HIP keeps memory after
+       a capture, which the differential leak test leaves out) */
+    const int max_flags = run_section("graph") ? DSR_BATCH_GRAPH : 0;
+    for (int flags = 0; flags <= max_flags; ++flags) {
+      dsr_batch* bt = NULL;
+      CHECK(dsr_batch_create_capacity(ctx, dec, &p, n_obj, mp, mr, flags, &bt) == 0, "%s", dsr_last_error(ctx));
+      CHECK(dsr_batch_run(bt) < 0, "run of an empty capacity batch accepted");
+      CHECK(dsr_batch_refill(bt, n_obj + 1, in) < 0, "refill beyond the object capacity accepted");
+      for (int r = 0; r < 4; ++r) {
+        const int back = r & 1;
+        CHECK(dsr_batch_refill(bt, n_obj, back ? rev : in) == 0, "%s", dsr_last_error(ctx));
+        memset(out, 0, osz);
+        CHECK(dsr_batch_run(bt) == 0, "%s", dsr_last_error(ctx));
+        CHECK(dsr_batch_download(bt, out) == 0, "%s", dsr_last_error(ctx));
+        for (int o = 0; o < n_obj; ++o)
+          CHECK(same_out(&ref[o], &out[back ? n_obj - 1 - o : o], 1), "capacity fill %d (flags %d) object %d", r,
+                flags, o);
+      }
+      dsr_stats st;
+      CHECK(dsr_batch_stats(bt, &st) == 0, "%s", dsr_last_error(ctx));
+      CHECK(st.graph_captures == (flags ? 1 : 0) && st.graph_replays == (flags ? 4 : 0), "captures %d replays %d",
+            st.graph_captures, st.graph_replays);
+      CHECK(dsr_batch_destroy(bt) == 0, "destroy");
+    }
+    dsr_batch* bt = NULL;
+    CHECK(dsr_batch_create(ctx, dec, &p, n_obj, in, &bt) == 0, "%s", dsr_last_error(ctx));
+    CHECK(dsr_batch_refill(bt, n_obj, in) < 0, "refill of an ordinary batch accepted");
+    CHECK(dsr_batch_destroy(bt) == 0, "destroy");
+    free(rev);
   }
 
   /* graph capture and replays */

@@ -105,6 +105,20 @@ class Decoder:
                                                      C.byref(h)), "dsr_decoder_load")
         self.handle = h
 
+    @property
+    def info(self):
+        """The load-time lite qualification (dsr_decoder_info_get) as a dict:
+        ``lite_eligible`` False means every batch on this decoder decodes exactly."""
+        import ctypes as C
+
+        from reconstruct import _libdsr as L
+
+        inf = L.DecoderInfo()
+        self.ctx.check(self.ctx.lib.dsr_decoder_info_get(self.handle, C.byref(inf)), "dsr_decoder_info_get")
+        d = {k: getattr(inf, k) for k, _ in inf._fields_}
+        d["lite_eligible"] = bool(d["lite_eligible"])
+        return d
+
     def __del__(self):
         try:
             if getattr(self, "handle", None):

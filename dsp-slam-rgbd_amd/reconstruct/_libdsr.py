@@ -67,7 +67,8 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 7          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 8          # include/dsr.h DSR_ABI_VERSION
+BATCH_GRAPH = 1          # include/dsr.h DSR_BATCH_GRAPH
 
 
 class Stats(C.Structure):
@@ -80,7 +81,17 @@ class Stats(C.Structure):
                 ("jac_render_points", C.c_int64), ("keep_masks", C.c_int),
                 ("lite_audit_violations", C.c_int), ("lite_redo_objects", C.c_int),
                 ("surface_in_exact", C.c_int), ("audit_points", C.c_int64),
-                ("lite_broken_blocks", C.c_int), ("test_hooks", C.c_int)]
+                ("lite_broken_blocks", C.c_int), ("test_hooks", C.c_int),
+                ("lite_eligible", C.c_int), ("audit", C.c_int), ("audit_shell", C.c_float),
+                ("audit_log2", C.c_int), ("lite_margin0", C.c_float), ("lite_floor", C.c_float),
+                ("lite_safety", C.c_float), ("graph_captures", C.c_int), ("graph_replays", C.c_int)]
+
+
+class DecoderInfo(C.Structure):
+    """dsr_decoder_info: the decoder's load-time lite qualification (include/dsr.h)."""
+    _fields_ = [("code_len", C.c_int), ("lite_eligible", C.c_int), ("lite_probe_ratio", C.c_double),
+                ("lite_probe_max_err", C.c_double), ("lite_probe_max_err_all", C.c_double),
+                ("probe_points", C.c_int), ("probe_codes", C.c_int), ("probe_ms", C.c_double)]
 
 #: dsr_batch_lite_diag record layout (csrc/dsr_dev.hpp: STD_*)
 LITE_DIAG_FIELDS = ("broken_blocks", "recorded", "block", "wave", "counter", "target", "observed", "tile_iter",
@@ -100,6 +111,7 @@ SIGNATURES = {
     "dsr_decoder_load": (C.c_int, [C.c_void_p, C.POINTER(DecoderDesc), FP, C.c_size_t,
                                    C.POINTER(C.c_void_p)]),
     "dsr_decoder_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsr_decoder_info_get": (C.c_int, [C.c_void_p, C.POINTER(DecoderInfo)]),
     "dsr_reconstruct_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int,
                                         C.POINTER(ObjectIn), C.POINTER(ObjectOut),
                                         C.POINTER(Trace)]),
@@ -113,6 +125,9 @@ SIGNATURES = {
     "dsr_batch_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "dsr_batch_lite_diag": (C.c_int, [C.c_void_p, IP, C.c_int]),
     "dsr_batch_destroy": (C.c_int, [C.c_void_p]),
+    "dsr_batch_create_capacity": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), C.c_int, C.c_int,
+                                            C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "dsr_batch_refill": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(ObjectIn)]),
     "dsr_sdf_eval": (C.c_int, [C.c_void_p, C.c_void_p, FP, FP, C.c_int, FP, FP]),
     "dsr_pose_only": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(OptimParams), FP, C.c_float,
                                 FP, C.c_int, FP, FP]),

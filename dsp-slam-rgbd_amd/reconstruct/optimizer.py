@@ -76,6 +76,11 @@ class Optimizer(object):
             int(self.num_iterations_joint_optim), int(self.code_len),
             int(self.num_depth_samples), float(self.cut_off), int(self.num_iterations_pose_only))
         self.last_stats = None
+        # keyframe stream (BASELINE config 5): "graph" = fixed-capacity slot batches refilled per
+        # keyframe, each replaying ONE captured hipGraph; "slot" = the same slots run eagerly;
+        # "oneshot" = a new batch per keyframe (dsr_batch_create)
+        self.keyframe_mode = os.environ.get("DSR_KEYFRAME_MODE", "graph")
+        self._slots = []
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -181,6 +186,38 @@ class Optimizer(object):
     def reconstruct_keyframe(self, detections):
         return self.reconstruct_keyframe_async(detections).wait()
 
+    MAX_SLOTS = 4
+
+    def _slot_for(self, objects):
+        """A free fixed-capacity batch (dsr_batch_create_capacity) that holds ``objects``, or
+        None (``keyframe_mode`` "oneshot", or every slot busy with an in-flight keyframe)."""
+        if self.keyframe_mode not in ("slot", "graph") or not objects:
+            return None
+        n = len(objects)
+        need_p = max(_f32(ob[1], 3).shape[0] for ob in objects)
+        need_r = max(_f32(ob[2], 3).shape[0] for ob in objects)
+        graph = self.keyframe_mode == "graph"
+        free = [sl for sl in self._slots if not sl.busy and sl.graph == graph]
+        for sl in free:
+            if sl.fits(n, need_p, need_r):
+                return sl
+        if free:                                     # grow the first free slot
+            old = free[0]
+            self._slots.remove(old)
+            old.close()
+            n, need_p, need_r = max(n, old.max_obj), max(need_p, old.max_pts), max(need_r, old.max_rays)
+        elif len(self._slots) >= self.MAX_SLOTS:
+            return None
+        sl = SlotBatch(self, n, -(-need_p // 128) * 128, -(-need_r // 128) * 128, graph)
+        self._slots.append(sl)
+        return sl
+
+    def close_slots(self):
+        """Release the keyframe slot batches (their device memory goes back to the context pool)."""
+        for sl in self._slots:
+            sl.close()
+        self._slots = []
+
     def estimate_pose_cam_obj(self, t_co_se3, scale, pts, code):
         """optimizer.py:46-87: pose-only SE(3) GN on the SDF term."""
         t = _f32(t_co_se3).reshape(4, 4)
@@ -255,14 +292,48 @@ class Optimizer(object):
         return float(mean_value)
 
 
-class BatchHandle:
-    """An in-flight batched reconstruction (Optimizer.reconstruct_objects_async)."""
+class SlotBatch:
+    """A fixed-capacity batch (dsr_batch_create_capacity) that keyframe after keyframe is
+    refilled (dsr_batch_refill) and re-run — with ``graph``, as replays of ONE hipGraph."""
 
-    def __init__(self, opt, objects):
+    def __init__(self, opt, max_obj, max_pts, max_rays, graph):
+        self.opt = opt
+        self.max_obj, self.max_pts, self.max_rays, self.graph = max_obj, max_pts, max_rays, graph
+        self.busy = False
+        ctx = opt._ctx
+        h = C.c_void_p()
+        ctx.check(ctx.lib.dsr_batch_create_capacity(ctx.handle, opt.decoder.handle, C.byref(opt.params), max_obj,
+                                                    max_pts, max_rays, L.BATCH_GRAPH if graph else 0, C.byref(h)),
+                  "dsr_batch_create_capacity")
+        self.handle = h
+
+    def fits(self, n, n_pts, n_rays):
+        return n <= self.max_obj and n_pts <= self.max_pts and n_rays <= self.max_rays
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h is not None:
+            try:
+                self.opt._ctx.lib.dsr_batch_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class BatchHandle:
+    """An in-flight batched reconstruction (Optimizer.reconstruct_objects_async); with a
+    ``slot`` (SlotBatch) the objects are refilled into that fixed-capacity batch instead of a
+    new batch being created."""
+
+    def __init__(self, opt, objects, slot=None):
         self.opt = opt
         self.n = len(objects)
         self._h = None
         self._res = None
+        self._slot = None
         if self.n == 0:
             self._res = []
             return
@@ -271,6 +342,13 @@ class BatchHandle:
         for i, ob in enumerate(objects):
             ins[i] = opt._object_in(*ob[:4], ob[4] if len(ob) > 4 else None, keep)
         ctx = opt._ctx
+        if slot is not None:
+            ctx.check(ctx.lib.dsr_batch_refill(slot.handle, self.n, ins), "dsr_batch_refill")
+            ctx.check(ctx.lib.dsr_batch_run(slot.handle), "dsr_batch_run")
+            slot.busy = True
+            self._slot = slot
+            self._h = slot.handle
+            return
         h = C.c_void_p()
         ctx.check(ctx.lib.dsr_batch_create(ctx.handle, opt.decoder.handle, C.byref(opt.params), self.n,
                                            ins, C.byref(h)), "dsr_batch_create")
@@ -298,8 +376,7 @@ class BatchHandle:
             try:
                 ctx.check(ctx.lib.dsr_batch_download(self._h, outs), "dsr_batch_download")
             finally:
-                ctx.lib.dsr_batch_destroy(self._h)
-                self._h = None
+                self._release()
             res = [Optimizer._result(outs[i]) for i in range(self.n)]
             for i in range(self.n):
                 res[i]["iters_done"] = int(outs[i].iters_done)
@@ -307,11 +384,20 @@ class BatchHandle:
             self._res = res
         return self._res
 
+    def _release(self):
+        if self._slot is not None:           # the slot batch stays; its next fill may start
+            self._slot.busy = False
+            self._slot = None
+        elif self._h is not None:
+            self.opt._ctx.lib.dsr_batch_destroy(self._h)
+        self._h = None
+
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None:
+        if getattr(self, "_h", None) is not None:
             try:
-                self.opt._ctx.lib.dsr_batch_destroy(h)
+                if self._slot is not None:   # an abandoned keyframe: finish its run before reuse
+                    self.opt._ctx.lib.dsr_batch_sync(self._h)
+                self._release()
             except Exception:
                 pass
 
@@ -335,7 +421,7 @@ class KeyframeHandle:
                 j = len(objs)
                 objs.append((np.asarray(t, np.float32).reshape(4, 4) @ FLIP, pts, rays, depth, code))
             self.pairs.append((i, j))
-        self.batch = BatchHandle(opt, objs)
+        self.batch = BatchHandle(opt, objs, opt._slot_for(objs))
 
     def done(self) -> bool:
         return self.batch.done()

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 7
+#define DSR_ABI_VERSION 8
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -146,7 +146,20 @@ typedef struct {
                                      expired in the last run (their samples all went to the
                                      exact pass: results stay exact, the cost rises); 0 expected */
   int test_hooks;                 /* 1: the batch was created with DSR_TEST_HOOKS=1, so the test
-                                     hooks DSR_LITE_PERTURB / DSR_LITE_BREAK were honoured */
+                                     hooks (DSR_LITE_PERTURB / _BREAK) and the lite-guard settings
+                                     below (DSR_LITE_AUDIT / _SHELL / _AUDIT_LOG2 / _MARGIN / _FLOOR /
+                                     _SAFETY) were read from the environment */
+  /* ---- the lite pass's guard as this batch ran it (ABI 8) ---- */
+  int lite_eligible;              /* the decoder passed its load-time lite qualification
+                                     (dsr_decoder_info); 0: every batch decodes exactly */
+  int audit;                      /* 1: audited out-of-band samples (lite_flag) */
+  float audit_shell;              /* certain audit of |y| < th + (1 + shell) * margin */
+  int audit_log2;                 /* plus a hashed 2^-audit_log2 share of all other samples */
+  float lite_margin0;             /* first-iteration margin */
+  float lite_floor;               /* later margins: max(floor, safety x largest observed error) */
+  float lite_safety;
+  int graph_captures;             /* hipGraph captures / replays over the batch's life */
+  int graph_replays;
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */
@@ -163,6 +176,29 @@ int dsr_device_count(int* n);
 int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* desc, const float* weights,
                      size_t n_floats, dsr_decoder** out);
 int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec);
+
+/* Load-time qualification of the one-product fp16 classification pass (no reference
+ * counterpart; it guards the build's replacement of decode_sdf, loss_utils.py:51-79, in the
+ * render term's occupancy classification, loss.py:98-102 / loss_utils.py:40-48).
+ * dsr_decoder_load decodes a fixed probe set — probe_points points uniform in the unit ball x
+ * probe_codes latent codes (zero, then N(0, s^2) per component for s = 0.1, 0.3, 1.0) — with
+ * the lite pass and with the exact split-fp16 pass and records, over every probe value, the
+ * largest |lite - exact| / max(floor, ||exact| - th|) (th = 0.01, floor = 0.002): the lite
+ * error as a fraction of the distance of the exact value to the nearest class boundary
+ * (full | band | empty), and the largest |lite - exact| near the surface (|exact| < 0.1).  A
+ * decoder whose ratio exceeds 0.5, or whose near-surface error exceeds half the floor (1e-3), is
+ * lite-ineligible: every batch on it decodes every ray sample exactly (the DSR_LITE=0 path,
+ * reported in dsr_stats). */
+typedef struct {
+  int code_len;
+  int lite_eligible;
+  double lite_probe_ratio;        /* max |lite - exact| / max(floor, ||exact| - th|) */
+  double lite_probe_max_err;      /* max |lite - exact| over probe values with |exact| < 0.1 */
+  double lite_probe_max_err_all;  /* max |lite - exact| over every probe value */
+  int probe_points, probe_codes;
+  double probe_ms;                /* host wall time of the qualification */
+} dsr_decoder_info;
+int dsr_decoder_info_get(const dsr_decoder* dec, dsr_decoder_info* info);
 
 /* ---- joint shape + pose GN: replaces Optimizer.reconstruct_object
  * (optimizer.py:90-205) for n_obj independent objects in one device pass.
@@ -191,6 +227,21 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st);
  * (csrc/dsr_dev.hpp: STD_*; 16 ints). */
 int dsr_batch_lite_diag(dsr_batch* b, int* rec, int n);
 int dsr_batch_destroy(dsr_batch* b);
+
+/* Fixed-capacity batches for a keyframe stream (BASELINE config 5; the per-keyframe loop
+ * LocalMapping_util.cc:256-445 / :165-206, overlapped with LocalMapping.cc:99-128): the batch
+ * is laid out once for max_obj objects of at most max_pts surface points and max_rays rays,
+ * and dsr_batch_refill uploads each keyframe's objects into those slots (host -> pinned
+ * staging -> one stream-ordered copy per input buffer) and rewrites the per-slot counts in
+ * device memory, so every kernel argument stays fixed.  With DSR_BATCH_GRAPH the whole GN run
+ * is captured as ONE hipGraph at the first run and every later run — after any refill —
+ * replays it (dsr_stats.graph_captures / graph_replays).  The batch starts empty; a run needs
+ * a refill first; dsr_batch_download returns the current fill's n_obj records.  A refill
+ * orders after the previous run's work on the context stream. */
+#define DSR_BATCH_GRAPH 1
+int dsr_batch_create_capacity(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int max_obj,
+                              int max_pts, int max_rays, int flags, dsr_batch** out);
+int dsr_batch_refill(dsr_batch* b, int n_obj, const dsr_object_in* in);
 
 /* ---- decoder queries: replaces decode_sdf / get_batch_sdf_jacobian
  * (loss_utils.py:51-113) as used by Optimizer.compute_sdf_loss_objectpoint_zhjd

@@ -53,7 +53,7 @@ def test_diag_library_exports_the_mfma_loop():
 
 STRUCTS = {"dsr_decoder_desc": "DecoderDesc", "dsr_optim_params": "OptimParams",
            "dsr_object_in": "ObjectIn", "dsr_object_out": "ObjectOut", "dsr_trace": "Trace",
-           "dsr_stats": "Stats", "dsr_pose_in": "PoseIn"}
+           "dsr_stats": "Stats", "dsr_pose_in": "PoseIn", "dsr_decoder_info": "DecoderInfo"}
 
 
 def test_struct_layouts_match_ctypes():
@@ -122,6 +122,8 @@ def test_c_stress_no_device_paths(exe_name):
     and against libdsr_asan.so (host code under AddressSanitizer + UBSan, leak checking
     on).  The device paths of the same driver run in test_gpu_api.py."""
     exe = os.path.join(REPO, "dsp-slam-rgbd_amd", "csrc", exe_name)
+    if exe_name.endswith("_asan") and not os.path.isfile(exe):
+        pytest.skip("host-sanitized build absent (make -C dsp-slam-rgbd_amd/csrc check)")
     assert os.path.isfile(exe), "built by make -C dsp-slam-rgbd_amd/csrc"
     p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr

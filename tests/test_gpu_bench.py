@@ -77,3 +77,34 @@ def test_bench_rccl_path_on_one_rank(tmp_path):
     assert "backend" not in one["ranks"]
     a, b = np.load(tmp_path / "rccl.npy"), np.load(tmp_path / "one.npy")
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_rehearse_the_driver_command(tmp_path):
+    """The driver's N = 8 command, rehearsed on one GPU: ``bench.py --gpus
+    8`` with no launcher spawns 8 ranks (gloo, all on device 0 — RCCL needs a GPU per rank),
+    each uploads its LPT shard of a 16-object job and of the config-4 leg (64 objects x 1024
+    points here, 8 per rank as at N = 8), one all-gather returns every record to rank 0 — and
+    both record sets are bitwise those of ``--gpus 1``."""
+    extra = ["--objects", "16", "--c4-objects", "64", "--c4-pts", "1024"]
+    args8 = [a for a in ARGS if a not in ("--no-config4",)]
+
+    def run(n, dump):
+        env = dict(os.environ, DSR_BENCH_BACKEND="gloo")
+        env.pop("WORLD_SIZE", None)
+        cmd = [sys.executable, "bench.py", "--gpus", str(n), *args8, *extra, "--dump-records", dump]
+        p = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=500)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return json.loads(p.stdout.strip().splitlines()[-1])
+
+    eight = run(8, str(tmp_path / "eight.npy"))
+    one = run(1, str(tmp_path / "one.npy"))
+    r = eight["ranks"]
+    assert eight["n_gpus"] == 8 and r["world_size_observed"] == 8 and r["backend"] == "gloo"
+    assert len(r["rank_seconds"]) == 8 and sorted(r["shard_objects"]) == [2] * 8
+    assert eight["config4"]["shard_objects"] == [8] * 8 and one["config4"]["shard_objects"] == [64]
+    for name in ("eight", "eight_c4"):
+        a, b = np.load(tmp_path / f"{name}.npy"), np.load(tmp_path / f"{name.replace('eight', 'one')}.npy")
+        assert a.shape == b.shape and a.shape[0] in (16, 64)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), name
+        assert (a[:, 1] == 1).all()

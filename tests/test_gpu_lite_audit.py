@@ -135,6 +135,7 @@ def test_audit_everything_mode(gpu_decoder, monkeypatch):
     as audits — and no class differs.  (Samples behind that one, decoded because they share its
     pass window, are not: transmittance is exactly 0 there, §3.3; ~9% of the lite samples.)"""
     monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
     monkeypatch.setenv("DSR_LITE_AUDIT_LOG2", "0")
     opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=3)
     objs = [S.kitti_object(i) for i in range(4)]
@@ -205,6 +206,76 @@ def test_test_hooks_ignored_without_the_gate(gpu_decoder, monkeypatch):
     assert st.lite_audit_violations == 0 and st.lite_broken_blocks == 0
     assert st.refine_points == st0.refine_points < st.fwd_points
     assert bytes(outs) == bytes(ref)
+
+
+GUARD_KNOBS = {"DSR_LITE_AUDIT": "0", "DSR_LITE_SHELL": "0", "DSR_LITE_AUDIT_LOG2": "24",
+               "DSR_LITE_MARGIN": "0.05", "DSR_LITE_FLOOR": "0.0001", "DSR_LITE_SAFETY": "0.5"}
+
+
+def test_guard_settings_ignored_without_the_gate(gpu_decoder, monkeypatch):
+    """The lite pass's guard is part of the product: without
+    DSR_TEST_HOOKS=1 the variables that would switch the audit off, drop its certain shell, thin
+    its hashed share or move the margin change nothing — bytes equal — and dsr_stats reports the
+    settings the batch actually ran with."""
+    f = golden("f4_traj_kitti0.npz")
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=3)
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e]) for e in (0, 4)]
+    monkeypatch.setenv("DSR_LITE", "1")
+    monkeypatch.delenv("DSR_TEST_HOOKS", raising=False)
+    for k in GUARD_KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    ref, st0 = batch_stats(opt, objs, pose_is_obj_cam=True)
+    for k, v in GUARD_KNOBS.items():
+        monkeypatch.setenv(k, v)
+    outs, st = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert bytes(outs) == bytes(ref)
+    for s in (st0, st):
+        assert s.test_hooks == 0 and s.lite == 1 and s.lite_eligible == 1
+        assert s.audit == 1 and s.audit_shell == 1.0 and s.audit_log2 == 7
+        assert abs(s.lite_margin0 - 0.01) < 1e-7 and abs(s.lite_floor - 0.002) < 1e-7 and s.lite_safety == 4.0
+    assert st.audit_points == st0.audit_points > 0
+    # under the gate the same variables do take effect (the survey / test paths)
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
+    _, sh = batch_stats(opt, objs, pose_is_obj_cam=True)
+    assert sh.test_hooks == 1 and sh.audit == 0 and sh.audit_points == 0 and sh.audit_shell == 0.0
+    assert abs(sh.lite_floor - 1e-4) < 1e-9 and sh.lite_safety == 0.5
+
+
+def test_bench_decoder_qualifies_for_the_lite_pass(gpu_decoder):
+    """dsr_decoder_load's probe (65,536 points in the unit ball x 4 codes, lite vs exact): the
+    bench decoder's lite error stays far inside half the distance to a class boundary."""
+    info = gpu_decoder.info
+    assert info["lite_eligible"], info
+    assert info["probe_points"] == 65536 and info["probe_codes"] == 4
+    assert 0.0 < info["lite_probe_ratio"] <= 0.5 and 0.0 < info["lite_probe_max_err"] <= 1e-3, info
+    print("\nbench decoder probe:", info)
+
+
+def test_high_error_decoder_routed_to_the_exact_path(monkeypatch):
+    """A deliberately high-error decoder (hidden-weight gain 5, against the bench decoder's
+    2.45: fp16 activations ~150x larger) fails the load-time qualification; every batch on it
+    runs the exact HIP path — the DSR_LITE=0 kernels, not the oracle — with results bytewise
+    those of DSR_LITE=0, also for warm-start codes of unit scale per component."""
+    from deep_sdf.workspace import decoder_from_state
+
+    dec = decoder_from_state(S.fit_last_layer_to_sphere(S.make_decoder_state(1234, hidden_gain=5.0)),
+                             S.DEFAULT_SPECS)
+    info = dec.info
+    assert not info["lite_eligible"] and info["lite_probe_max_err"] > 1e-3, info
+    print("\ngain-5 decoder probe:", info)
+    opt = _opt(dec, S.KITTI_OPTIM, iters=2)
+    rng = np.random.default_rng(5)
+    objs = []
+    for i, scale in enumerate((0.0, 1.0)):
+        o = S.kitti_object(i)
+        objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, (scale * rng.standard_normal(64)).astype(np.float32)))
+    monkeypatch.delenv("DSR_LITE", raising=False)
+    outs, st = batch_stats(opt, objs)
+    assert st.lite == 0 and st.lite_eligible == 0 and st.refine_points == 0 and st.fwd_points > 0
+    monkeypatch.setenv("DSR_LITE", "0")
+    ref, st0 = batch_stats(opt, objs)
+    assert bytes(outs) == bytes(ref)
+    assert st.fwd_points == st0.fwd_points
 
 
 def _violating_batch(opt, objs, monkeypatch):

@@ -216,6 +216,39 @@ def test_batch_equals_single(gpu_decoder, streams, monkeypatch):
             assert np.array_equal(tr[i][key], tr1[0][key]), (i, key)
 
 
+def test_default_schedules_give_bitwise_equal_results(gpu_decoder, monkeypatch):
+    """the default render-pass schedule depends on the batch's sample
+    count, ray count and the device's CU count — so an object alone (one KITTI object: windows
+    14,24), in an 8-object shard (16,24), in a 16-object frame (8,12,16,20,24,32) or decoded in
+    ONE pass gets a different schedule.  None of this may change a bit of its result: the lite
+    values are per sample, every sample in front of a ray's first certainly-full one is decoded
+    under every schedule, and the exact pass re-decodes exactly those flagged in front of it
+    (band, audit shell and the hashed audits: k_refine_scan stops there), so its tiles — and
+    their split-fp16 scales — are the same list under every schedule."""
+    monkeypatch.delenv("DSR_RENDER_PASSES", raising=False)
+    monkeypatch.delenv("DSR_STREAMS", raising=False)
+    opt = _opt(gpu_decoder, dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=3)),
+               "KITTI")
+    objs = [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in (S.kitti_object(i) for i in range(16))]
+    runs = {"batch16": opt.reconstruct_objects(objs, trace=True),
+            "batch8": opt.reconstruct_objects(objs[:8], trace=True)}
+    singles = [opt.reconstruct_objects([ob], trace=True) for ob in objs[:3]]
+    monkeypatch.setenv("DSR_RENDER_PASSES", "0")
+    runs["one_pass"] = opt.reconstruct_objects(objs[:8], trace=True)
+    ref_res, ref_tr = runs["batch8"]
+    cases = [("batch16", runs["batch16"], range(8)), ("one_pass", runs["one_pass"], range(8))]
+    cases += [(f"single{i}", singles[i], [i]) for i in range(len(singles))]
+    for name, (res, tr), idx in cases:
+        for j, i in enumerate(idx):
+            a, b = res[j], ref_res[i]
+            assert a["is_good"] == b["is_good"] and a["loss"] == b["loss"], (name, i)
+            if a["is_good"]:
+                assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"]), (name, i)
+                assert np.array_equal(a["code"], b["code"]), (name, i)
+            for key in ("H", "b", "n_valid", "k"):
+                assert np.array_equal(tr[j][key], ref_tr[i][key]), (name, i, key)
+
+
 def test_failure_cases(gpu_decoder):
     f = golden("f6_fail.npz")
     opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")

@@ -23,12 +23,13 @@ def _free_port():
     return p
 
 
-def _objects():
+def _objects(n=5, ragged=True):
     import synthetic as S
 
     objs = []
-    for i in range(5):
-        o = S.make_object(500 + i, n_pts=40 + 13 * i, n_bg=10 + 7 * i, scale=1.0, tz=3.0, upright=False)
+    for i in range(n):
+        k = i if ragged else 0
+        o = S.make_object(500 + i, n_pts=40 + 13 * k, n_bg=10 + 7 * k, scale=1.0, tz=3.0, upright=False)
         objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
     return objs
 
@@ -142,7 +143,7 @@ def _fake_optimizer():
     return Optimizer(Dec(), cfg)
 
 
-def _resident_worker(rank, world, port, q):
+def _resident_worker(rank, world, port, q, n_obj=5):
     import sys
 
     for p in (PKG, REPO):
@@ -155,7 +156,7 @@ def _resident_worker(rank, world, port, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        shard = ResidentShard(_fake_optimizer(), _objects())
+        shard = ResidentShard(_fake_optimizer(), _objects(n_obj, ragged=n_obj == 5))
         first = shard.run()
         second = shard.run()                 # inputs stay resident: a re-run gives the same records
         shard.launch()                       # bench.py's overlapped steps: step s+1 launched
@@ -205,6 +206,36 @@ def test_resident_shard_world2_equals_one_process():
             assert np.array_equal(np.asarray(T, np.float32), np.asarray(r["t_cam_obj"], np.float32))
 
 
+@pytest.mark.timeout(600)
+def test_resident_shard_world8_equals_one_process():
+    """The driver's N = 8 path on CPU: 8 gloo ranks, one 64-object job of
+    equal-cost objects — LPT gives every rank 8 (BASELINE config 4's split) — each rank uploads
+    and runs only its shard, one all-gather returns every record to rank 0 in input order,
+    bitwise the one-process ResidentShard's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resident_worker, args=(r, 8, port, q, 64)) for r in range(8)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=500)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from reconstruct.parallel import ResidentShard
+
+    ref = ResidentShard(_fake_optimizer(), _objects(64, ragged=False)).run()
+    assert [len(s) for s in got["shards"]] == [8] * 8 and len(got["mine"]) == 8
+    assert sorted(i for s in got["shards"] for i in s) == list(range(64))
+    assert got["same"] and got["gather"] > 0.0
+    assert len(got["res"]) == len(ref) == 64
+    for (good, loss, T, it), r in zip(got["res"], ref):
+        assert good == r["is_good"] and it == r["iters_done"]
+        assert np.float32(loss) == np.float32(r["loss"])
+        if good:
+            assert np.array_equal(np.asarray(T, np.float32), np.asarray(r["t_cam_obj"], np.float32))
+
+
 def test_bench_spawns_its_own_ranks(monkeypatch):
     """`python bench.py --gpus N` without a launcher starts torch.distributed.run with N local
     ranks as a child process (no exec of a process that touched the GPU)."""
@@ -228,6 +259,12 @@ def test_bench_spawns_its_own_ranks(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
         bench.main()
+    # under a launcher WITHOUT --gpus (torchrun --nproc-per-node 8 bench.py): the launcher's ranks
+    # are taken; only an explicit, disagreeing --gpus is an error
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "2"])
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    args, world = bench.parse_args()
+    assert args.gpus == 2 == world
 
 
 def test_lpt_partition_balances_and_covers():
