@@ -383,10 +383,12 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   if (!ctx || !d || !w || !out) return fail(ctx, "null argument");
   *out = nullptr;
   // The topology DSP-SLAM ships (deep_sdf_decoder.py with dims=[512]*8, latent_in=[4],
-  // weight_norm, no xyz_in_all, no use_tanh).  Anything else is rejected loudly.
-  static const int od[9] = {512, 512, 512, 445, 512, 512, 512, 512, 1};
-  static const int id[9] = {67, 512, 512, 512, 512, 512, 512, 512, 512};
-  if (d->code_len != CODE) return fail(ctx, "libdsr supports code_len == 64 only");
+  // weight_norm, no xyz_in_all, no use_tanh) at CodeLength 64 or 32 (LocalMapping_util.cc:416-422
+  // handles both).  Anything else is rejected loudly.
+  if (d->code_len != 64 && d->code_len != 32) return fail(ctx, "libdsr supports code_len 64 or 32");
+  const int L = d->code_len, l3 = HID - (L + 3);           // lin3 out: 445 / 477
+  const int od[9] = {512, 512, 512, l3, 512, 512, 512, 512, 1};
+  const int id[9] = {L + 3, 512, 512, 512, 512, 512, 512, 512, 512};
   if (d->n_layers != 9) return fail(ctx, "libdsr supports the 9-layer (dims=[512]*8) DeepSDF decoder only");
   for (int i = 0; i < 9; ++i)
     if (d->out_dim[i] != od[i] || d->in_dim[i] != id[i])
@@ -405,6 +407,17 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   hipSetDevice(ctx->device);
 
   auto Wat = [&](int l, int r, int c) { return W[l][(size_t)r * id[l] + c]; };
+  // Everything downstream uses the 64-D layout: a 32-D decoder's code columns 32..63 are zero
+  // (its J_code entries there are exactly 0, H's code block there k3 I, its step 0: the 39-
+  // parameter system of the reference, solved inside the 71 one).  lin4's input is [h3 (l3) |
+  // code (L) | xyz (3)]; the GEMMs see h3 | xyz, K4 = l3 + 3 deep (448 / 480), the code is
+  // folded into the per-object bias.
+  const int K4 = l3 + 3, K3b = (l3 + 31) / 32 * 32;
+  auto E0 = [&](int r, int c) {            // lin0 in the 64-D layout: [code (64) | xyz (3)]
+    return c < CODE ? (c < L ? Wat(0, r, c) : 0.f) : Wat(0, r, L + (c - CODE));
+  };
+  auto A3 = [&](int r, int c) { return r < l3 ? Wat(3, r, c) : 0.f; };
+  auto A4 = [&](int r, int c) { return c < l3 ? Wat(4, r, c) : (c < K4 ? Wat(4, r, l3 + L + (c - l3)) : 0.f); };
   std::vector<std::vector<float>> blobs;
   std::vector<size_t> offs;
   size_t total = 0;
@@ -421,11 +434,9 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 1; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 3) {
-      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return r < L3_OUT ? Wat(3, r, c) : 0.f; });
+      sw16[l] = pack_frag16(v16, 512, 512, A3);
     } else if (l == 4) {
-      sw16[l] = pack_frag16(v16, 512, 448, [&](int r, int c) {
-        return c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
-      });
+      sw16[l] = pack_frag16(v16, 512, K4, A4);
     } else {
       sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); });
     }
@@ -437,7 +448,7 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   // rescale multiply (same lane layout as pack_frag16's hi pieces, packed densely)
   int hl16[8] = {-1};
   for (int l = 1; l <= 7; ++l) {
-    const int K = (l == 4) ? 448 : 512, T = K / 32;
+    const int K = (l == 4) ? K4 : 512, T = K / 32;
     std::vector<_Float16> v16((size_t)32 * T * 64 * 8);
     for (int rb = 0; rb < 32; ++rb)
       for (int t = 0; t < T; ++t)
@@ -445,8 +456,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
           for (int j = 0; j < 8; ++j) {
             const int r = 16 * rb + (lane & 15), c = 32 * t + 8 * (lane >> 4) + j;
             float x;
-            if (l == 3) x = r < L3_OUT ? Wat(3, r, c) : 0.f;
-            else if (l == 4) x = c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
+            if (l == 3) x = A3(r, c);
+            else if (l == 4) x = A4(r, c);
             else x = Wat(l, r, c);
             v16[(((size_t)rb * T + t) * 64 + lane) * 8 + j] = (_Float16)x;
           }
@@ -458,12 +469,10 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
     std::vector<float> v;
     if (l == 3) {
       Kf[l] = 512;
-      pack_frag(v, 512, 512, [&](int r, int c) { return r < L3_OUT ? Wat(3, r, c) : 0.f; });
+      pack_frag(v, 512, 512, A3);
     } else if (l == 4) {
-      Kf[l] = 448;
-      pack_frag(v, 512, 448, [&](int r, int c) {
-        return c < L3_OUT ? Wat(4, r, c) : Wat(4, r, L3_OUT + CODE + (c - L3_OUT));
-      });
+      Kf[l] = K4;
+      pack_frag(v, 512, K4, A4);
     } else {
       Kf[l] = 512;
       pack_frag(v, 512, 512, [&](int r, int c) { return Wat(l, r, c); });
@@ -474,9 +483,9 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 0; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 0) {
-      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? Wat(0, c, r) : 0.f; });
+      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; });
     } else if (l == 3) {
-      swb16[l] = pack_frag16(v16, 512, 448, [&](int r, int c) { return c < L3_OUT ? Wat(3, c, r) : 0.f; });
+      swb16[l] = pack_frag16(v16, 512, K3b, [&](int r, int c) { return A3(c, r); });
     } else {
       swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); });
     }
@@ -487,8 +496,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 1; l <= 7; ++l) {
     std::vector<float> v;
     if (l == 3) {
-      Kb[l] = 448;
-      pack_frag(v, 512, 448, [&](int r, int c) { return c < L3_OUT ? Wat(3, c, r) : 0.f; });
+      Kb[l] = K3b;
+      pack_frag(v, 512, K3b, [&](int r, int c) { return A3(c, r); });
     } else {
       Kb[l] = 512;
       pack_frag(v, 512, 512, [&](int r, int c) { return Wat(l, c, r); });
@@ -498,7 +507,7 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   {
     std::vector<float> v;
     Kb[0] = 512;
-    pack_frag(v, 80, 512, [&](int r, int c) { return r < IN ? Wat(0, c, r) : 0.f; });
+    pack_frag(v, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; });
     hb[0] = add(std::move(v));
   }
   for (int l = 0; l <= 7; ++l) {
@@ -508,10 +517,10 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   }
   std::vector<float> w0x(512 * 3), w0z(512 * 64), w4z(512 * 64), w8(512);
   for (int n = 0; n < 512; ++n) {
-    for (int i = 0; i < 3; ++i) w0x[n * 3 + i] = Wat(0, n, CODE + i);
+    for (int i = 0; i < 3; ++i) w0x[n * 3 + i] = Wat(0, n, L + i);
     for (int k = 0; k < 64; ++k) {
-      w0z[k * 512 + n] = Wat(0, n, k);          // k-major: the fold's loads coalesce over n
-      w4z[k * 512 + n] = Wat(4, n, L3_OUT + k);
+      w0z[k * 512 + n] = k < L ? Wat(0, n, k) : 0.f;          // k-major: the fold's loads coalesce over n
+      w4z[k * 512 + n] = k < L ? Wat(4, n, l3 + k) : 0.f;
     }
     w8[n] = Wat(8, 0, n);
   }
@@ -520,6 +529,7 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
 
   auto* dec = new dsr_decoder();
   dec->ctx = ctx;
+  dec->code_len = L;
   dec->bytes = total * sizeof(float);
   if (hipMalloc(&dec->dmem, dec->bytes) != hipSuccess) {
     delete dec;
@@ -547,6 +557,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   D.W4z = P(h4z);
   D.W8 = P(h8);
   D.b8 = B[8][0];
+  D.code_len = L;
+  D.l3 = l3;
   for (int l = 0; l < 8; ++l) {
     D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
     D.Wl_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hl16[l])) : nullptr;
@@ -767,7 +779,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     if (x.n_pts > 0) hpts.insert(hpts.end(), x.pts, x.pts + (size_t)x.n_pts * 3);
     if (x.n_rays > 0) hrays.insert(hrays.end(), x.rays, x.rays + (size_t)x.n_rays * 3);
     for (int r = 0; r < x.n_rays; ++r) hdobs.push_back(r < x.n_depth ? x.depth[r] : 0.f);
-    if (x.code) std::copy(x.code, x.code + CODE, hz.begin() + (size_t)o * CODE);
+    if (x.code) std::copy(x.code, x.code + dec->code_len, hz.begin() + (size_t)o * CODE);   // (rest 0)
     std::copy(x.t_cam_obj, x.t_cam_obj + 16, ht.begin() + (size_t)o * 16);
     hoc[o] = x.pose_is_obj_cam ? 1 : 0;
     const int cap = x.n_rays * M;
@@ -1034,8 +1046,8 @@ int dsr_batch_refill(dsr_batch* b, int n_obj, const dsr_object_in* in) {
     float* t = t_in + (size_t)o * 16;
     for (int i = 0; i < 16; ++i) t[i] = x ? x->t_cam_obj[i] : (i % 5 == 0 ? 1.f : 0.f);
     float* z = z_in + (size_t)o * CODE;
-    if (x && x->code) std::memcpy(z, x->code, sizeof(float) * CODE);
-    else std::memset(z, 0, sizeof(float) * CODE);
+    std::memset(z, 0, sizeof(float) * CODE);
+    if (x && x->code) std::memcpy(z, x->code, sizeof(float) * b->dec->code_len);
     is_oc[o] = (x && x->pose_is_obj_cam) ? 1 : 0;
     if (!x) continue;
     if (x->n_pts) std::memcpy(pts + (size_t)d.pts_off * 3, x->pts, sizeof(float) * 3 * x->n_pts);
@@ -1506,7 +1518,7 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
           if (t.sdf_loss) t.sdf_loss[e] = v[2 * NPAR + 1];
           if (t.render_loss) t.render_loss[e] = v[2 * NPAR + 2];
           if (t.t_obj_cam) std::memcpy(t.t_obj_cam + (size_t)e * 16, v + 2 * NPAR + 3, sizeof(float) * 16);
-          if (t.z) std::memcpy(t.z + (size_t)e * CODE, v + 2 * NPAR + 19, sizeof(float) * CODE);
+          if (t.z) std::memcpy(t.z + (size_t)e * dec->code_len, v + 2 * NPAR + 19, sizeof(float) * dec->code_len);
           if (t.n_valid) t.n_valid[e] = I[k * 2];
           if (t.k) t.k[e] = I[k * 2 + 1];
         }
@@ -1790,7 +1802,10 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
   const DevDecoder& D = m->dec->D;
-  DSR_CHECK(ctx, hipMemcpyAsync(m->code, code, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
+  float zc[CODE] = {};                               // a 32-D code runs padded with zeros
+  std::memcpy(zc, code, sizeof(float) * m->dec->code_len);
+  DSR_CHECK(ctx, hipMemcpyAsync(m->code, zc, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
+  DSR_CHECK(ctx, hipStreamSynchronize(s));          // (zc is on this stack frame)
   hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)m->code, m->b0, m->b4);
   hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
@@ -1857,6 +1872,8 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   if (n <= 0) return 0;
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
+  float zc[CODE] = {};                               // a 32-D code runs padded with zeros
+  std::memcpy(zc, code, sizeof(float) * dec->code_len);
   const int nt = (n + TILE - 1) / TILE;
   std::vector<float4> hp((size_t)nt * TILE, make_float4(0.f, 0.f, 0.f, 0.f));
   for (int i = 0; i < n; ++i) {
@@ -1885,7 +1902,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
     return fail(ctx, "hipMalloc failed (sdf_eval)");
   }
   bool ok = hipMemcpy(dp, hp.data(), sizeof(float4) * hp.size(), hipMemcpyHostToDevice) == hipSuccess &&
-            hipMemcpy(dz, code, sizeof(float) * CODE, hipMemcpyHostToDevice) == hipSuccess &&
+            hipMemcpy(dz, zc, sizeof(float) * CODE, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(dt, ht.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(dnt, &nt, sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
             hipMemcpy(dd, &d, sizeof(ObjDesc), hipMemcpyHostToDevice) == hipSuccess;
@@ -1914,10 +1931,14 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   ok = hipMemcpy(h.data(), dout, sizeof(float) * h.size(), hipMemcpyDeviceToHost) == hipSuccess;
   cleanup();
   if (!ok) return fail(ctx, "hipMemcpy D2H failed (sdf_eval)");
+  // jac rows: [code (code_len) | xyz (3)] (the kernels' 64-D layout holds code 0..63, xyz 64..66)
+  const int L = dec->code_len, jw = L + 3;
   for (int i = 0; i < n; ++i) {
     sdf[i] = h[i * outw];
-    if (jac)
-      for (int k = 0; k < IN; ++k) jac[(size_t)i * IN + k] = h[i * outw + 1 + k];
+    if (jac) {
+      for (int k = 0; k < L; ++k) jac[(size_t)i * jw + k] = h[i * outw + 1 + k];
+      for (int k = 0; k < 3; ++k) jac[(size_t)i * jw + L + k] = h[i * outw + 1 + CODE + k];
+    }
   }
   return 0;
 }
@@ -1946,7 +1967,7 @@ int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_pa
     for (int i = 0; i < 16; ++i) t_in[16 * o + i] = x.t_co_se3[i];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) t_in[16 * o + i * 4 + j] = t_in[16 * o + i * 4 + j] * x.scale;   // :56 (fp32)
-    std::copy(x.code, x.code + CODE, hz.begin() + (size_t)CODE * o);
+    std::copy(x.code, x.code + dec->code_len, hz.begin() + (size_t)CODE * o);   // (rest 0)
     hp[o].assign(x.pts, x.pts + (size_t)x.n_pts * 3);
     cap_pts += x.n_pts;
     cap_tiles += (x.n_pts + TILE - 1) / TILE;

@@ -55,7 +55,16 @@ struct DevDecoder {
   // split-fp16 backward A-fragments of lin_l^T (l = 1..7; [0] = lin0^T, 80 rows), scale 2^swb[l]
   const _Float16* Wbh_raw[8];
   int swb[8];
+  // code length (64 or 32; a 32-D decoder runs in the 64-D layout with its code columns 32..63 of
+  // lin0 / lin4 zero and its code held at zero there) and lin3's output count l3 = 509 - code_len
+  // (445 / 477): lin4's input is [h3 (l3) | code | xyz], so its xyz rows are l3..l3+2 — wave
+  // l3 >> 6, 16-row block (l3 >> 4) & 3, quad g = 3, rows r = 1..3 (l3 % 16 == 13 for both)
+  int code_len;
+  int l3;
 };
+
+// d sdf / d[code, xyz] slot (gin, 64-D layout: code 0..63, xyz 64..66) of lin4's input row n >= l3
+__device__ __forceinline__ int gin_slot(int n, int l3) { return n < HID - 3 ? n - l3 : CODE + (n - (HID - 3)); }
 
 struct ObjDesc {
   int pts_off, n_pts;    // into pts

@@ -721,7 +721,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
       const int T = D.Kf[l] / 16;
       fwd_gemm<V>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
-      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mask, l == 3);
+      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mask, l == 3, D.l3);
       __syncthreads();
     }
     {
@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
       const int T = D.Kf[l] / 16;
       jac_gemm<JV>(D.Wf[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
-      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mk[l], l == 3);
+      epi_fwd(acc, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm.H, sm.xyz, w, lane, mk[l], l == 3, D.l3);
       __syncthreads();
     }
     {
@@ -1135,7 +1135,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
       const int T = D.Kb[l] / 16;
       jac_gemm<JV>(D.Wb[l] + (size_t)(4 * w) * T * 64, T, sm.H, acc, lane);
       __syncthreads();
-      if (l == 4) epi_bwd_l4(acc, sm.H, sm.gin, w, lane, mk[3]);
+      if (l == 4) epi_bwd_l4(acc, sm.H, sm.gin, w, lane, mk[3], D.l3, D.Kb[3]);
       else epi_bwd(acc, sm.H, w, lane, mk[l - 1]);
       __syncthreads();
     }
@@ -1150,7 +1150,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * w + 4 * g + r;
-          if (n < IN) sm.gin[p * GIN_PITCH + n] = accr(a1[0][cb], r) + sm.gin[p * GIN_PITCH + n];
+          // (a code_len-32 decoder: code slots 32..63 have zero weights and no lin4 part: 0)
+          if (n < IN)
+            sm.gin[p * GIN_PITCH + n] = accr(a1[0][cb], r) + ((n >= D.code_len && n < CODE) ? 0.f : sm.gin[p * GIN_PITCH + n]);
         }
       }
     }
@@ -1349,7 +1351,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           }
         }
         mk[l] = bits;
-        if (l == 3 && w == 6) xyz_rows(v, sm.xyz, lane, m);     // lin4 input = h3 | xyz
+        if (l == 3 && w == (D.l3 >> 6)) xyz_rows(v, sm.xyz, lane, m, (D.l3 >> 4) & 3);   // lin4 input = h3 | xyz
         JSTAMP(2)
         fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
@@ -1430,10 +1432,10 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           m = fmaxf(m, fabsf(gv));
         }(), ...);
       }(std::make_integer_sequence<int, 64>{});
-      if (l == 4 && w >= 6) {
-        // d/d[code, xyz] via the latent skip: lin3^T's input rows n >= 445 are lin4's code and
-        // xyz columns (wave 7: rows 448..511 all; wave 6: rows 445..447 = q 3, g 3, r 1..3).
-        // Their gradient goes to gin, and they carry no ReLU (mask bit 0 for them: zeroed)
+      if (l == 4 && w >= (D.l3 >> 6)) {
+        // d/d[code, xyz] via the latent skip: lin3^T's input rows n >= l3 (445 at code_len 64:
+        // wave 7 all, wave 6 rows 445..447) are lin4's code and xyz columns.  Their gradient
+        // goes to gin (gin_slot), and they carry no ReLU (mask bit 0 for them: zeroed)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1442,11 +1444,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int n = 64 * w + 16 * q + 4 * g + r;
-              if (w == 7 || (q == 3 && r > 0)) {
-                if (n >= L3_OUT) {
-                  sm.gin[p * GIN_PITCH + (n - L3_OUT)] = accr(acc[q][cb], r) * usc;
-                  v[q][cb][r] = 0.f;
-                }
+              if (n >= D.l3) {
+                sm.gin[p * GIN_PITCH + gin_slot(n, D.l3)] = accr(acc[q][cb], r) * usc;
+                v[q][cb][r] = 0.f;
               }
             }
           }
@@ -1472,7 +1472,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = 16 * w + 4 * g + r;
-          if (n < IN) sm.gin[p * GIN_PITCH + n] = ldexpf(accr(a1[0][cb], r), -un) + sm.gin[p * GIN_PITCH + n];
+          if (n < IN)
+            sm.gin[p * GIN_PITCH + n] =
+                ldexpf(accr(a1[0][cb], r), -un) + ((n >= D.code_len && n < CODE) ? 0.f : sm.gin[p * GIN_PITCH + n]);
         }
       }
     }

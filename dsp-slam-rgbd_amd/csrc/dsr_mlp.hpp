@@ -174,7 +174,7 @@ __device__ __forceinline__ void layer0_fwd(const DevDecoder& D, const float* __r
 // columns of lin4's 448-deep input (the 64 code columns are folded into bias4).
 __device__ __forceinline__ void epi_fwd(floatx4 (&acc)[4][4], const float* __restrict__ bias,
                                         float* Hs, const float* __restrict__ xyz, int w,
-                                        int lane, uint64_t& mask, bool is_l3) {
+                                        int lane, uint64_t& mask, bool is_l3, int l3) {
   const int g = lane >> 4, c = lane & 15;
   mask = 0;
 #pragma unroll
@@ -190,7 +190,7 @@ __device__ __forceinline__ void epi_fwd(floatx4 (&acc)[4][4], const float* __res
         v[r] = relu_t(accr(acc[q][cb], r) + fetch4(bb, r));
         if (relu_pass(v[r])) mask |= 1ull << ((q * 4 + cb) * 4 + r);
       }
-      if (is_l3 && n0 == 444) {          // rows 445,446,447 <- x,y,z
+      if (is_l3 && n0 == l3 - 1) {       // rows l3..l3+2 (445..447 at code_len 64) <- x,y,z
         v[1] = xyz[p * 4 + 0];
         v[2] = xyz[p * 4 + 1];
         v[3] = xyz[p * 4 + 2];
@@ -254,7 +254,7 @@ __device__ __forceinline__ void epi_bwd(floatx4 (&acc)[4][4], float* Hs, int w, 
 // 445..447 are zeroed (they are K padding of the lin3^T GEMM).
 constexpr int GIN_PITCH = 68;
 __device__ __forceinline__ void epi_bwd_l4(floatx4 (&acc)[4][4], float* Hs, float* gin, int w,
-                                           int lane, uint64_t mask3) {
+                                           int lane, uint64_t mask3, int l3, int kb3) {
   const int g = lane >> 4, c = lane & 15;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -267,14 +267,14 @@ __device__ __forceinline__ void epi_bwd_l4(floatx4 (&acc)[4][4], float* Hs, floa
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + r;
         const float a = accr(acc[q][cb], r);
-        if (n < L3_OUT) {
+        if (n < l3) {
           v[r] = ((mask3 >> ((q * 4 + cb) * 4 + r)) & 1ull) ? a : 0.f;
         } else {
           v[r] = 0.f;
-          gin[p * GIN_PITCH + (n - L3_OUT)] = a;
+          gin[p * GIN_PITCH + gin_slot(n, l3)] = a;
         }
       }
-      if (n0 < 448)
+      if (n0 < kb3)
         *reinterpret_cast<float4*>(Hs + p * PITCH + n0) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }

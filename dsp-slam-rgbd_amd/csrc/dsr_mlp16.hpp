@@ -449,20 +449,25 @@ __device__ __forceinline__ uint64_t relu_bits(const float (&v)[4][4][4]) {
   return mk;
 }
 
-// lin4's input is h3 | xyz: lin3's padded output rows 445..447 (wave 6, q 3, g 3, r 1..3)
-// carry the point's x, y, z.  Called under a wave-uniform branch (w == 6); the row choice
-// is a per-lane select, not a per-element divergent branch.  m takes their magnitudes.
+// lin4's input is h3 | xyz: lin3's padded output rows l3..l3+2 (445..447 at code_len 64: wave 6,
+// q 3, g 3, r 1..3; 477..479 at 32: wave 7, q 1) carry the point's x, y, z.  Called under a
+// wave-uniform branch (w == l3 >> 6) with the wave-uniform block xq; the row choice is a per-lane
+// select, not a per-element divergent branch.  m takes their magnitudes.
 template <int NCB>
-__device__ __forceinline__ void xyz_rows(float (&v)[4][NCB][4], const float* xyz, int lane, float& m) {
+__device__ __forceinline__ void xyz_rows(float (&v)[4][NCB][4], const float* xyz, int lane, float& m, int xq) {
   const int g = lane >> 4, c = lane & 15;
-  const bool on = g == 3;
 #pragma unroll
-  for (int cb = 0; cb < NCB; ++cb) {
-    const float4 p = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
-    v[3][cb][1] = on ? p.x : v[3][cb][1];
-    v[3][cb][2] = on ? p.y : v[3][cb][2];
-    v[3][cb][3] = on ? p.z : v[3][cb][3];
-    m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+  for (int q = 0; q < 4; ++q) {               // the xyz rows' 16-row block: a wave-uniform choice
+    if (q != xq) continue;
+    const bool on = g == 3;
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+      const float4 p = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+      v[q][cb][1] = on ? p.x : v[q][cb][1];
+      v[q][cb][2] = on ? p.y : v[q][cb][2];
+      v[q][cb][3] = on ? p.z : v[q][cb][3];
+      m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+    }
   }
 }
 
@@ -474,7 +479,7 @@ struct NoStamp {
 template <class Stamp = NoStamp>
 __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
                                          Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk,
-                                         Stamp stamp = Stamp{}) {
+                                         int l3, Stamp stamp = Stamp{}) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
@@ -497,7 +502,7 @@ __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, cons
       }
     }
   }
-  if (is_l3 && w == 6) xyz_rows(v, sm.xyz, lane, m);
+  if (is_l3 && w == (l3 >> 6)) xyz_rows(v, sm.xyz, lane, m, (l3 >> 4) & 3);
   stamp(2);
   const Scales2 sc = block_scale2(m, sm.wmax, w, lane);   // all waves done reading H
   stamp(3);
@@ -610,7 +615,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
       uint64_t mk;
-      sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, stamp);
+      sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, D.l3,
+                 stamp);
       if constexpr (MSK) mask_push(mq, mk);
       stamp(7);
       __syncthreads();

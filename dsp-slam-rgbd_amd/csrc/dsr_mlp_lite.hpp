@@ -352,15 +352,20 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
           }
         }
       }
-      if (l == 3 && w == 6) {   // lin4 input = h3 | xyz: rows 445..447 (q 3, g 3, r 1..3) <- x, y, z
+      if (l == 3 && w == (D.l3 >> 6)) {   // lin4 input = h3 | xyz: rows l3..l3+2 (g 3, r 1..3) <- x, y, z
+        const int xq = (D.l3 >> 4) & 3;
 #pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
-          const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
-          const bool on = g == 3;
-          acc[3][cb][1] = on ? p.x : acc[3][cb][1];
-          acc[3][cb][2] = on ? p.y : acc[3][cb][2];
-          acc[3][cb][3] = on ? p.z : acc[3][cb][3];
-          m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+        for (int q = 0; q < 4; ++q) {
+          if (q != xq) continue;
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
+            const bool on = g == 3;
+            acc[q][cb][1] = on ? p.x : acc[q][cb][1];
+            acc[q][cb][2] = on ? p.y : acc[q][cb][2];
+            acc[q][cb][3] = on ? p.z : acc[q][cb][3];
+            m = fmaxf(m, on ? fmaxf(fabsf(p.x), fmaxf(fabsf(p.y), fabsf(p.z))) : 0.f);
+          }
         }
       }
       sa = lite_scale<LV>(m, sm.wmax, &sm.ovf, w, lane);
@@ -487,6 +492,9 @@ __device__ __forceinline__ void st_expire(int* c, int target, int observed, Lite
 }
 
 __device__ __forceinline__ void st_report(const LiteStShared& sm, int* diag, int w) {
+#ifdef DSR_EXP_NODIAG   // traffic experiment: round 2's wait without the expired-wait record
+  return;
+#endif
   if (diag == nullptr || sm.rec[4] != w || __lane_id() != 0) return;
   atomicAdd(diag + STD_BROKEN, 1);
   if (atomicCAS(diag + STD_CLAIM, 0, 1) != 0) return;
@@ -511,11 +519,18 @@ __device__ __forceinline__ void st_wait(int* c, int target, LiteStShared& sm, in
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&sm.broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
       break;
     ++n;
+#ifdef DSR_EXP_NODIAG
+    if (n > (1 << DSR_LITE_WAIT_LOG2)) {
+      __hip_atomic_store(&sm.broken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+#else
     if (n == 1024) sm.twait[w] = (unsigned)__builtin_amdgcn_s_memrealtime();   // a long wait: clock it
     if (n > (1 << DSR_LITE_WAIT_LOG2)) {
       st_expire(c, target, v, sm, it, w);
       break;
     }
+#endif
     __builtin_amdgcn_s_sleep(1);
   }
   asm volatile("" ::: "memory");
@@ -698,15 +713,20 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
             for (int r = 0; r < 4; ++r) h[r] = (_Float16)v[r];
             hv[q][cb] = __builtin_elementwise_max(h, half4{0, 0, 0, 0});
           }
-        if (l == 3 && w == 6) {   // lin4 input rows 445..447 <- x, y, z (after the ReLU)
+        if (l == 3 && w == (D.l3 >> 6)) {   // lin4 input rows l3..l3+2 <- x, y, z (after the ReLU)
+          const int xq = (D.l3 >> 4) & 3;
 #pragma unroll
-          for (int cb = 0; cb < 8; ++cb) {
-            const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
-            const bool on = g == 3;
-            hv[3][cb][1] = on ? (_Float16)pt.x : hv[3][cb][1];
-            hv[3][cb][2] = on ? (_Float16)pt.y : hv[3][cb][2];
-            hv[3][cb][3] = on ? (_Float16)pt.z : hv[3][cb][3];
-            mi = max(mi, on ? __float_as_int(fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z)))) : 0);
+          for (int q = 0; q < 4; ++q) {
+            if (q != xq) continue;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+              const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+              const bool on = g == 3;
+              hv[q][cb][1] = on ? (_Float16)pt.x : hv[q][cb][1];
+              hv[q][cb][2] = on ? (_Float16)pt.y : hv[q][cb][2];
+              hv[q][cb][3] = on ? (_Float16)pt.z : hv[q][cb][3];
+              mi = max(mi, on ? __float_as_int(fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z)))) : 0);
+            }
           }
         }
         if (!(__int_as_float(mi) < 32768.f)) sm.ovf[p] = it + 1;
@@ -743,15 +763,20 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           }
         }
       }
-      if (l == 3 && w == 6) {   // lin4 input = h3 | xyz: rows 445..447 (q 3, g 3, r 1..3) <- x, y, z
+      if (l == 3 && w == (D.l3 >> 6)) {   // lin4 input = h3 | xyz: rows l3..l3+2 (g 3, r 1..3) <- x, y, z
+        const int xq = (D.l3 >> 4) & 3;
 #pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
-          const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
-          const bool on = g == 3;
-          acc[3][cb][1] = on ? pt.x : acc[3][cb][1];
-          acc[3][cb][2] = on ? pt.y : acc[3][cb][2];
-          acc[3][cb][3] = on ? pt.z : acc[3][cb][3];
-          m = fmaxf(m, on ? fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z))) : 0.f);
+        for (int q = 0; q < 4; ++q) {
+          if (q != xq) continue;
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            const float4 pt = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
+            const bool on = g == 3;
+            acc[q][cb][1] = on ? pt.x : acc[q][cb][1];
+            acc[q][cb][2] = on ? pt.y : acc[q][cb][2];
+            acc[q][cb][3] = on ? pt.z : acc[q][cb][3];
+            m = fmaxf(m, on ? fmaxf(fabsf(pt.x), fmaxf(fabsf(pt.y), fabsf(pt.z))) : 0.f);
+          }
         }
       }
       if (!(m < 32768.f)) sm.ovf[p] = it + 1;
@@ -807,12 +832,16 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           const ObjState& So = E.st[tl.obj];
           const float margin = So.lite_margin;
           y = lite_perturb(E, y, idx);
+#ifndef DSR_EXP_NOOUT   // traffic experiment (invalid results): no per-sample outputs
           dense[d.cand_off + idx] = y;
           bool full = false;
           const unsigned char fl = (sm.ovf[p] == it + 1 || sm.broken)
                                        ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
           if (fl) E.refine[d.cand_off + idx] = fl;               // band / range guard / audit
           if (fl != 1 && full) E.dead[d.ray_off + idx / E.M] = 1;  // certainly full
+#else
+          if (y == 12345.f) dense[d.cand_off + idx] = margin;
+#endif
         }
       }
       st_signal(&sm.cE);

@@ -64,10 +64,11 @@ def check_topology(specs, layers):
         raise NotImplementedError("use_tanh decoders are not supported by libdsr")
     if list(ns.get("latent_in", [])) != [4]:
         raise NotImplementedError("libdsr supports latent_in=[4] only")
-    if specs["CodeLength"] != 64:
-        raise NotImplementedError("libdsr supports CodeLength=64 only")
+    L = specs["CodeLength"]
+    if L not in (64, 32):
+        raise NotImplementedError("libdsr supports CodeLength 64 or 32")
     shapes = [W.shape for W, _ in layers]
-    want = [(512, 67)] + [(512, 512)] * 2 + [(445, 512)] + [(512, 512)] * 4 + [(1, 512)]
+    want = [(512, L + 3)] + [(512, 512)] * 2 + [(509 - L, 512)] + [(512, 512)] * 4 + [(1, 512)]
     if shapes != want:
         raise NotImplementedError(f"unsupported decoder shapes {shapes}")
 

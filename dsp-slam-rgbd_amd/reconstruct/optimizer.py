@@ -106,10 +106,12 @@ class Optimizer(object):
         return rec
 
     @staticmethod
-    def _result(o):
+    def _result(o, code_len=64):
+        """An out-record as the reference's result dict; ``code`` holds code_len values (the
+        record's 64-wide code carries a 32-D code in its first 32, LocalMapping_util.cc:416-422)."""
         if o.is_good:
             return ForceKeyErrorDict(t_cam_obj=np.ctypeslib.as_array(o.t_cam_obj).reshape(4, 4).copy(),
-                                     code=np.ctypeslib.as_array(o.code).copy(),
+                                     code=np.ctypeslib.as_array(o.code)[:code_len].copy(),
                                      is_good=True, loss=float(o.loss))
         return ForceKeyErrorDict(t_cam_obj=None, code=None, is_good=False, loss=float(o.loss))
 
@@ -155,7 +157,7 @@ class Optimizer(object):
                   "dsr_reconstruct_batch")
         if _VERBOSE:
             print("Reconstruction takes %f seconds" % (time.time() - t0))
-        res = [self._result(outs[i]) for i in range(n)]
+        res = [self._result(outs[i], self.code_len) for i in range(n)]
         for i in range(n):
             res[i]["iters_done"] = int(outs[i].iters_done)
             res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")
@@ -277,7 +279,7 @@ class Optimizer(object):
         ctx = decoders[0].ctx
         ctx.check(ctx.lib.dsr_reconstruct_multi(ctxs, decs, nd, C.byref(self.params), n, ins, outs),
                   "dsr_reconstruct_multi")
-        res = [self._result(outs[i]) for i in range(n)]
+        res = [self._result(outs[i], self.code_len) for i in range(n)]
         for i in range(n):
             res[i]["iters_done"] = int(outs[i].iters_done)
             res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")
@@ -377,7 +379,7 @@ class BatchHandle:
                 ctx.check(ctx.lib.dsr_batch_download(self._h, outs), "dsr_batch_download")
             finally:
                 self._release()
-            res = [Optimizer._result(outs[i]) for i in range(self.n)]
+            res = [Optimizer._result(outs[i], self.opt.code_len) for i in range(self.n)]
             for i in range(self.n):
                 res[i]["iters_done"] = int(outs[i].iters_done)
                 res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")

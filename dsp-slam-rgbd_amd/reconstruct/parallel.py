@@ -9,8 +9,8 @@ returns the fixed-size result records to rank 0.
 * partitioning: longest-processing-time-first on the estimated cost
   ``n_rays * M + n_pts`` (decoder work of one iteration), greedy to the least loaded
   rank — per-object cost varies with the ray count;
-* record: 96 float32 = t_cam_obj[16] | code[64] | loss | is_good | iters_done |
-  object index | 12 pad; ranks pad to the largest shard so one fixed-size
+* record: 96 float32 = t_cam_obj[16] | code[64] (a 32-D code: its 32 values, then zeros) |
+  loss | is_good | iters_done | object index | 12 pad; ranks pad to the largest shard so one fixed-size
   ``all_gather_into_tensor`` moves everything (~25 KB for 64 objects).
 """
 from __future__ import annotations
@@ -42,7 +42,8 @@ def pack(results, indices):
     for k, (r, i) in enumerate(zip(results, indices)):
         if r["is_good"]:
             rec[k, :16] = np.asarray(r["t_cam_obj"], np.float32).reshape(-1)
-            rec[k, 16:80] = np.asarray(r["code"], np.float32)
+            c = np.asarray(r["code"], np.float32).reshape(-1)
+            rec[k, 16:16 + c.shape[0]] = c
         rec[k, 80] = r["loss"]
         rec[k, 81] = 1.0 if r["is_good"] else 0.0
         rec[k, 82] = float(r.get("iters_done", -1))
@@ -50,12 +51,12 @@ def pack(results, indices):
     return rec
 
 
-def unpack(rec):
+def unpack(rec, code_len=64):
     from reconstruct.utils import ForceKeyErrorDict
 
     good = rec[81] > 0.5
     return ForceKeyErrorDict(t_cam_obj=rec[:16].reshape(4, 4).copy() if good else None,
-                             code=rec[16:80].copy() if good else None, is_good=bool(good),
+                             code=rec[16:16 + code_len].copy() if good else None, is_good=bool(good),
                              loss=float(rec[80]), iters_done=int(rec[82]))
 
 
@@ -74,12 +75,12 @@ def gather_records(rec, width, group=None, device=None):
     return out.cpu().numpy() if dist.get_rank(group) == 0 else None
 
 
-def unpack_all(allrec, n):
+def unpack_all(allrec, n, code_len=64):
     results = [None] * n
     for row in allrec:
         i = int(row[83])
         if i >= 0:
-            results[i] = unpack(row)
+            results[i] = unpack(row, code_len)
     return results
 
 
@@ -137,7 +138,7 @@ class ResidentShard:
         rec = np.zeros((self.width, REC), np.float32)
         rec[:, 83] = -1.0
         if self.handle is not None:
-            res = [self.opt._result(self.outs[k]) for k in range(len(self.mine))]
+            res = [self.opt._result(self.outs[k], self.opt.code_len) for k in range(len(self.mine))]
             for k, r in enumerate(res):
                 r["iters_done"] = int(self.outs[k].iters_done)
             rec[:len(self.mine)] = pack(res, self.mine)
@@ -152,11 +153,11 @@ class ResidentShard:
         rec = self.pack_records()
         if not self.dist:
             self.last_gather_s = 0.0
-            return unpack_all(rec, self.n)
+            return unpack_all(rec, self.n, self.opt.code_len)
         t0 = time.perf_counter()
         allrec = gather_records(rec, self.width, self.group, self.device)
         self.last_gather_s = time.perf_counter() - t0
-        return None if allrec is None else unpack_all(allrec, self.n)
+        return None if allrec is None else unpack_all(allrec, self.n, self.opt.code_len)
 
     def run(self):
         """One step: launch, wait, gather. Results in input order on rank 0, None elsewhere."""
@@ -176,7 +177,7 @@ class ResidentShard:
             pass
 
 
-def reconstruct_sharded(objects, solve, group=None, device=None, n_depth_samples=50):
+def reconstruct_sharded(objects, solve, group=None, device=None, n_depth_samples=50, code_len=64):
     """Reconstruct ``objects`` (list of ``(t_cam_obj, pts, rays, depth, code)``) across the
     ranks of ``group``; every rank passes the same list.  ``solve(list) -> list of
     result dicts`` runs one shard (normally ``Optimizer.reconstruct_objects``).
@@ -194,4 +195,4 @@ def reconstruct_sharded(objects, solve, group=None, device=None, n_depth_samples
     if mine:
         rec[:len(mine)] = pack(res, mine)
     allrec = gather_records(rec, width, group, device)     # one RCCL collective over xGMI
-    return None if allrec is None else unpack_all(allrec, len(objects))
+    return None if allrec is None else unpack_all(allrec, len(objects), code_len)

@@ -397,7 +397,10 @@ def test_c_stress_leaks_nothing_beyond_the_runtime(gpu_decoder, tmp_path):
         return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
 
     every = leaked("graph")
-    none = leaked("graph,trace,resident,redo,multi,query,mesher,errors,capacity")
+    # the runtime's own count varies from run to run by one allocation (r4a: 115 / 116 with no
+    # section, 6,600 / 6,648 B; r4b: 116 both ways, the capacity section alone included), so
+    # the reference is the larger of two runs without any section
+    none = max(leaked("graph,trace,resident,redo,multi,query,mesher,errors,capacity") for _ in range(2))
     # the same number of unattributed runtime allocations, and no more bytes beyond a few
     # dozen: the runtime's own blocks vary by a few bytes with the path taken (DSR_STREAMS=1:
     # 6,648 B with every section vs 6,672 B with none, 116 allocations both)

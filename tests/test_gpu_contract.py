@@ -210,3 +210,78 @@ def test_full_size_ensemble_matches_reference_ensemble(gpu_decoder, name, optim,
               f"{np.quantile(g_err[:, k], 0.9):.2e} ref {np.quantile(r_err[:, k], 0.9):.2e}")
         assert g_err[:, k].max() <= 1.25 * r_err[:, k].max(), c
         assert np.quantile(g_err[:, k], 0.9) <= 1.5 * np.quantile(r_err[:, k], 0.9), c
+
+
+def test_unperturbed_run_inside_the_reference_envelope(gpu_decoder):
+    """next to the distribution tests, the canonical (unperturbed) run at full size
+    — the metric object, golden F4 kitti0 / kitti5 — lands within 2x the reference
+    ensemble's envelope: each of its rotation / translation / code / loss deviations from the
+    reference's unperturbed result at most twice the largest deviation among the reference's
+    own 64 ulp-perturbed members (make_ensemble.py: ens64_*)."""
+    from reconstruct.optimizer import Optimizer
+
+    opt = Optimizer(gpu_decoder, make_cfg(S.KITTI_OPTIM, "KITTI"))
+    for name in ("kitti0", "kitti5"):
+        f = golden(f"f4_traj_{name}.npz")
+        (r,) = opt.reconstruct_objects([(f["obj_t_cam_obj"], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)])
+        assert r["is_good"]
+        g = np.array(contract_errors(r["t_cam_obj"], r["code"], r["loss"], f))
+        env = np.array([contract_errors(f[ENS + "t_cam_obj"][m], f[ENS + "code"][m], f[ENS + "loss"][m], f)
+                        for m in range(f[ENS + "loss"].shape[0])]).max(0)
+        print(f"\n{name}: unperturbed GPU rot/t/code/loss {np.array2string(g, precision=2)} "
+              f"vs reference envelope {np.array2string(env, precision=2)}")
+        assert (g <= 2.0 * env).all(), (g, env)
+
+
+def test_ens256_distribution_per_iteration(gpu_decoder):
+    """the metric object (F4 kitti0: KITTI params, 2048 pts x 2248 rays x 10
+    iterations) from the 256 ulp-perturbed starts of the reference's golden F13 ensemble
+    (tests/golden/make_ens256.py, 1 thread each), all in ONE GPU batch.  At n = 256 a two-sample
+    KS test at p = 1e-3 rejects a gap of D > ~0.17 (n = 64: ~0.34).  Compared:
+    * per iteration, the render-point count K and the pre-update loss k1*render + k2*sdf
+      (loss.py:22-43, :60-166; optimizer.py:157): KS p >= 1e-3 and loss means within 3 standard
+      errors of their difference — the clouds evolve alike, not only end alike;
+    * final rotation / translation / code / loss deviations from the reference's unperturbed
+      result: KS p >= 1e-3, medians within 2x, final-loss means within 3 SE."""
+    from scipy.stats import ks_2samp
+
+    from reconstruct.optimizer import Optimizer
+
+    f = golden("f4_traj_kitti0.npz")
+    e256 = golden("f13_ens256_kitti0.npz")
+    t_init = e256["t_init"]
+    n = t_init.shape[0]
+    assert n == 256 and bool(np.all(e256["is_good"]))
+    opt = Optimizer(gpu_decoder, make_cfg(S.KITTI_OPTIM, "KITTI"))
+    res, tr = opt.reconstruct_objects([(t_init[m], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)
+                                       for m in range(n)], trace=True)
+    assert all(r["is_good"] for r in res)
+    jo = S.KITTI_OPTIM["joint_optim"]
+    n_it = int(f["n_iters_run"])
+    worst = 1.0
+    for e in range(n_it):
+        kg = np.array([t["k"][e] for t in tr], np.float64)
+        kr = e256["it_k"][:, e].astype(np.float64)
+        lg = np.array([t["loss"][e] for t in tr], np.float64)
+        lr = jo["k1"] * e256["it_render_loss"][:, e] + jo["k2"] * e256["it_sdf_loss"][:, e]
+        pk = ks_2samp(kg, kr).pvalue if (kg.std() > 0 or kr.std() > 0 or kg[0] != kr[0]) else 1.0
+        pl = ks_2samp(lg, lr).pvalue
+        se = np.sqrt((lg.var(ddof=1) + lr.var(ddof=1)) / n)
+        print(f"it {e}: K mean gpu {kg.mean():.1f} ref {kr.mean():.1f} (KS p {pk:.3f}); loss mean gpu "
+              f"{lg.mean():.6f} ref {lr.mean():.6f} |d| {abs(lg.mean() - lr.mean()):.2e} 3SE {3 * se:.2e} (KS p {pl:.3f})")
+        assert pk >= 1e-3 and pl >= 1e-3, (e, pk, pl)
+        assert abs(lg.mean() - lr.mean()) <= 3 * se + 1e-12, e
+        worst = min(worst, pk, pl)
+    g_err = np.array([contract_errors(r["t_cam_obj"], r["code"], r["loss"], f) for r in res])
+    r_err = np.array([contract_errors(e256["t_cam_obj"][m], e256["code"][m], e256["loss"][m], f) for m in range(n)])
+    g_loss, r_loss = np.array([r["loss"] for r in res], np.float64), e256["loss"].astype(np.float64)
+    for k, c in enumerate(("rot", "t", "code", "loss")):
+        p = ks_2samp(g_err[:, k], r_err[:, k]).pvalue
+        med = np.median(g_err[:, k]) / max(np.median(r_err[:, k]), 1e-30)
+        print(f"final {c}: deviation median gpu {np.median(g_err[:, k]):.2e} ref {np.median(r_err[:, k]):.2e} "
+              f"(ratio {med:.2f}) KS p {p:.3f}")
+        assert p >= 1e-3 and 0.5 <= med <= 2.0, (c, p, med)
+        worst = min(worst, p)
+    se = np.sqrt((g_loss.var(ddof=1) + r_loss.var(ddof=1)) / n)
+    assert abs(g_loss.mean() - r_loss.mean()) <= 3 * se
+    print(f"smallest KS p over {n_it} iterations x (K, loss) + 4 final marginals: {worst:.3f}")

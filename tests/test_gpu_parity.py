@@ -130,14 +130,69 @@ def test_teacher_forced_iterations_vs_golden(gpu_decoder, name, optim, dtype):
         edx = rel(t["dx"][0], f["it_dx"][e])
         print(f"{name} it {e}: dK {dk} H {eh:.2e} b {eb:.2e} b(all) {eb_rot:.2e} dx(H-norm) {es:.2e} dx {edx:.2e}")
         # measured (r2, every F4 state): identical K -> H <= 1.2e-4, b <= 1.4e-4; one flipped
-        # render point -> H <= 2.4e-4, b <= 1.5e-3; b with the prior entries <= 1.3e-2,
-        # dx <= 9.9e-3 in the H-norm and 1.7e-2 max-normalised (both at kitti5 it 9, whose
-        # b[3:6] cancellation is the largest)
+        # render point -> H <= 2.4e-4, b <= 1.5e-3; dx <= 9.9e-3 in the H-norm.  b[3:6] and dx
+        # max-normalised are held against the fp64 truth below
+        # (test_teacher_forced_steps_no_less_accurate_than_the_reference)
         assert eh <= (5e-4 if dk == 0 else 2e-3), (e, eh)
         assert eb <= (5e-4 if dk == 0 else 5e-3), (e, eb)
-        assert eb_rot <= 5e-2, e
         assert es <= 1e-2, e
-        assert edx <= 5e-2, e
+
+
+@pytest.mark.parametrize("name,optim,dtype", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),
+                                              ("redwood1", S.REDWOOD_OPTIM, "Redwood"),
+                                              ("kitti0", S.KITTI_OPTIM, "KITTI"),
+                                              ("kitti5", S.KITTI_OPTIM, "KITTI"),
+                                              ("kitti4096", S.KITTI_OPTIM, "KITTI")])
+def test_teacher_forced_steps_no_less_accurate_than_the_reference(gpu_decoder, name, optim, dtype):
+    """from every recorded reference state, the GPU's b — in particular
+    b[3:6], where the rotation prior puts k4 = 1e7 times an fp32 cancellation (r_rot = 1 - cos
+    of the tilt, /root/reference/reconstruct/loss.py:169-192, optimizer.py:176-181) — and its
+    step dx are measured against the fp64 truth of the same step (golden F14: the oracle in
+    float64 from that state, tests/golden/make_fp64_truth.py), and so is the reference's own fp32
+    b / dx (F4 it_b / it_dx).  At every iteration whose render set K agrees in all three, the
+    GPU's error must stay within 2x the reference's own plus one fp32 rounding of the
+    entry's scale, and over the trajectory its RMS error within 1.25x the reference's."""
+    f = golden(f"f4_traj_{name}.npz")
+    t64 = golden(f"f14_fp64_{name}.npz")
+    one = dict(optim, joint_optim=dict(optim["joint_optim"], num_iterations=1))
+    opt = _opt(gpu_decoder, one, dtype)
+    n_it = int(f["n_iters_run"])
+    objs = [(f["it_t_obj_cam"][e], f["obj_pts"], f["obj_rays"], f["obj_depth"], f["it_z"][e])
+            for e in range(n_it)]
+    res, tr = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
+    eps = 2.0 ** -23
+    acc = {k: [] for k in ("b_rot", "b_rest", "dx", "dx_H")}
+    used = 0
+    for e in range(n_it):
+        kg, kr, k64 = int(tr[e]["k"][0]), int(f["it_k"][e]), int(t64["k"][e])
+        if not (kg == kr == k64):
+            print(f"{name} it {e}: K gpu {kg} ref {kr} fp64 {k64} (skipped: different render sets)")
+            continue
+        used += 1
+        b64, dx64, H64 = (np.asarray(t64[k][e], np.float64) for k in ("b", "dx", "H"))
+        rows = []
+        for key, sl in (("b_rot", np.s_[3:6]), ("b_rest", np.r_[0:3, 6:71])):
+            sc = np.abs(b64[sl]).max()
+            eg = np.abs(np.asarray(tr[e]["b"][0], np.float64)[sl] - b64[sl]).max() / sc
+            er = np.abs(np.asarray(f["it_b"][e], np.float64)[sl] - b64[sl]).max() / sc
+            acc[key].append((eg, er))
+            rows.append(f"{key} gpu {eg:.2e} ref {er:.2e}")
+        sc = np.abs(dx64).max()
+        eg = np.abs(np.asarray(tr[e]["dx"][0], np.float64) - dx64).max() / sc
+        er = np.abs(np.asarray(f["it_dx"][e], np.float64) - dx64).max() / sc
+        acc["dx"].append((eg, er))
+        hg = step_err(tr[e]["dx"][0], dx64, H64)
+        hr = step_err(f["it_dx"][e], dx64, H64)
+        acc["dx_H"].append((hg, hr))
+        print(f"{name} it {e}: " + "  ".join(rows) + f"  dx gpu {eg:.2e} ref {er:.2e}  dx(H) gpu {hg:.2e} ref {hr:.2e}")
+    assert used >= max(1, n_it // 2), (used, n_it)
+    for key, v in acc.items():
+        a = np.array(v)
+        for e_gpu, e_ref in a:
+            assert e_gpu <= 2.0 * e_ref + 4 * eps, (key, e_gpu, e_ref)
+        rms_g, rms_r = np.sqrt((a[:, 0] ** 2).mean()), np.sqrt((a[:, 1] ** 2).mean())
+        print(f"{name} {key}: RMS error vs fp64 gpu {rms_g:.2e} ref {rms_r:.2e}")
+        assert rms_g <= 1.25 * rms_r + 4 * eps, (key, rms_g, rms_r)
 
 
 @pytest.mark.parametrize("name,optim,dtype", [("redwood0", S.REDWOOD_OPTIM, "Redwood"),

@@ -275,6 +275,11 @@ def test_unsupported_decoder_variants_rejected_loudly(change, what):
     with pytest.raises(NotImplementedError, match=what):
         check_topology(specs, layers)
     specs = copy.deepcopy(S.DEFAULT_SPECS)
-    specs["CodeLength"] = 32
+    specs["CodeLength"] = 48
     with pytest.raises(NotImplementedError, match="CodeLength"):
         check_topology(specs, layers)
+    # CodeLength 32 is supported (LocalMapping_util.cc:416-422), with its own layer shapes
+    specs["CodeLength"] = 32
+    with pytest.raises(NotImplementedError, match="shapes"):
+        check_topology(specs, layers)
+    check_topology(specs, fold_state(S.make_decoder(1234, specs), specs))

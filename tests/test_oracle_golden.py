@@ -272,3 +272,44 @@ def test_oracle_edge_cases_f10(oracle_dec):
     T = O.estimate_pose_cam_obj(oracle_dec, Pk, f["pose_t_se3"], float(f["pose_scale"]), f["obj_pts"][:0], z)
     assert np.isnan(T).all() and np.isnan(f["pose_empty_out"]).all()
     assert np.isnan(O.compute_sdf_loss_objectpoint(oracle_dec, f["obj_pts"][:0], z)) and np.isnan(f["zhjd_empty_out"])
+
+
+SPECS32 = dict(S.DEFAULT_SPECS, CodeLength=32)
+KITTI32 = dict(S.KITTI_OPTIM, code_len=32, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=3))
+
+
+def test_oracle_code32_decoder_and_steps():
+    """Golden F15 (tests/golden/make_code32.py: the REFERENCE with a CodeLength-32 decoder,
+    /root/reference/src/LocalMapping_util.cc:416-422): the regenerated 32-D decoder folds to the
+    reference's weights bit for bit, the oracle's sdf / Jacobian (35 columns) match its
+    get_batch_sdf_jacobian, and one oracle GN step from each recorded reference state matches
+    its 39-parameter H / b / dx and losses."""
+    import hashlib
+
+    from deep_sdf.workspace import fold_state
+
+    f = golden("f15_code32.npz")
+    layers = fold_state(S.make_decoder(1234, SPECS32), SPECS32)
+    h = hashlib.sha256()
+    for W, b in layers:
+        h.update(W.tobytes())
+        h.update(b.tobytes())
+    assert h.hexdigest() == str(f["folded_sha256"])
+    assert [W.shape for W, _ in layers][0] == (512, 35) and layers[3][0].shape == (477, 512)
+    dec = O.Decoder(layers, 32, (4,))
+    y, j = dec.forward_jac(np.concatenate([np.broadcast_to(f["z"], (256, 32)), f["x"]], 1))
+    assert np.abs(y - f["sdf"]).max() <= 2e-6
+    assert_jac_close(j, f["jac"], tol=2e-5)
+    P = O.OptimParams.from_cfg(KITTI32)
+    n_fg = f["obj_depth"].shape[0]
+    dobs = np.concatenate([f["obj_depth"], np.zeros(f["obj_rays"].shape[0] - n_fg)]).astype(np.float32)
+    jo = KITTI32["joint_optim"]
+    assert f["it_H"].shape[1:] == (39, 39)
+    for e in range(int(f["n_iters_run"])):
+        tr, _, _ = O.gn_step(dec, P, f["it_t_obj_cam"][e], f["it_z"][e], f["obj_pts"], f["obj_rays"], dobs, n_fg)
+        assert abs(tr.k - f["it_k"][e]) <= 2
+        loss_ref = jo["k1"] * f["it_render_loss"][e] + jo["k2"] * f["it_sdf_loss"][e]
+        assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref)
+        assert tr.H.shape == (39, 39)
+        assert rel(tr.H, f["it_H"][e]) <= 3e-3
+        assert rel(tr.b, f["it_b"][e]) <= 1e-2
