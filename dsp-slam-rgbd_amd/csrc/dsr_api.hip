@@ -410,14 +410,16 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   // Everything downstream uses the 64-D layout: a 32-D decoder's code columns 32..63 are zero
   // (its J_code entries there are exactly 0, H's code block there k3 I, its step 0: the 39-
   // parameter system of the reference, solved inside the 71 one).  lin4's input is [h3 (l3) |
-  // code (L) | xyz (3)]; the GEMMs see h3 | xyz, K4 = l3 + 3 deep (448 / 480), the code is
-  // folded into the per-object bias.
-  const int K4 = l3 + 3, K3b = (l3 + 31) / 32 * 32;
+  // code (L) | xyz (3)]; the GEMMs see h3 | xyz, K4 deep (448 = 445 + 3; 512 >= 477 + 3), the code
+  // is folded into the per-object bias.
+  // (the GEMM k loops are unrolled for 14 or 16 k steps: lin4's h3 | xyz depth and lin3^T's depth
+  // pad to 448 or 512 — zero weights over the ReLU'd zero rows of lin3's padded outputs)
+  const int K4 = l3 + 3 <= 448 ? 448 : 512, K3b = l3 <= 448 ? 448 : 512;
   auto E0 = [&](int r, int c) {            // lin0 in the 64-D layout: [code (64) | xyz (3)]
     return c < CODE ? (c < L ? Wat(0, r, c) : 0.f) : Wat(0, r, L + (c - CODE));
   };
   auto A3 = [&](int r, int c) { return r < l3 ? Wat(3, r, c) : 0.f; };
-  auto A4 = [&](int r, int c) { return c < l3 ? Wat(4, r, c) : (c < K4 ? Wat(4, r, l3 + L + (c - l3)) : 0.f); };
+  auto A4 = [&](int r, int c) { return c < l3 ? Wat(4, r, c) : (c < l3 + 3 ? Wat(4, r, l3 + L + (c - l3)) : 0.f); };
   std::vector<std::vector<float>> blobs;
   std::vector<size_t> offs;
   size_t total = 0;

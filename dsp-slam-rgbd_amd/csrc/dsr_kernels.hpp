@@ -1634,23 +1634,32 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       S.fail_reason = f;
     } else {
       scal[0] = P.k1 * ren_loss + P.k2 * sdf_loss;                 // :157
-      // rotation prior, loss.py:169-192, at the current (pre-update) pose
-      float rco[16];
-      for (int i = 0; i < 16; ++i) rco[i] = S.Tco[i];
-      const float sc = powf(det3(rco), 0.33333334f);
-      float r3[9], roc[9];
+      // rotation prior, loss.py:169-192, at the current (pre-update) pose.  Evaluated in fp64
+      // from the fp32 inverse(T) (the reference's own t_cam_obj, same getrf/getrs as :122):
+      // res_rot = 1 + R_co[1][1] is a cancellation ~1e-5 that k4 = 1e7 multiplies into b[3:6],
+      // and the fp32 chain det -> pow(1/3) -> divide puts ~1e-7 of noise into R_co[1][1]
+      // (1% of res_rot) — in the reference as much as here; fp64 removes it
+      // (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_the_reference)
+      double r3[9];
       for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) r3[i * 3 + j] = rco[i * 4 + j] / sc;
-      inv_small<3>(r3, roc);
-      const float res_rot = 1.f - (-r3[1 * 3 + 1]);              // 1 - (R_co e_y).n_g
+        for (int j = 0; j < 3; ++j) r3[i * 3 + j] = (double)S.Tco[i * 4 + j];
+      auto det = [](const double* m) {
+        return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+               m[2] * (m[3] * m[7] - m[4] * m[6]);
+      };
+      const double sc = cbrt(det(r3));
+      for (int i = 0; i < 9; ++i) r3[i] /= sc;
+      const double dr = det(r3);
+      const double res_rot = 1.0 - (-r3[1 * 3 + 1]);             // 1 - (R_co e_y).n_g
       for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
-      if (res_rot < 1e-7f) {
+      if (res_rot < 1e-7) {
         scal[1] = 0.f;
       } else {
-        jrot[3] = roc[2 * 3 + 1];                                   // (R_oc n_g) x e_y
+        // (R_oc n_g) x e_y = (R_oc[2][1], 0, -R_oc[0][1]), R_oc = adj(R_co) / det(R_co)
+        jrot[3] = (float)((r3[0 * 3 + 1] * r3[2 * 3 + 0] - r3[0 * 3 + 0] * r3[2 * 3 + 1]) / dr);   // R_oc[2][1]
         jrot[4] = 0.f;
-        jrot[5] = -roc[0 * 3 + 1];
-        scal[1] = res_rot;
+        jrot[5] = (float)(-(r3[0 * 3 + 2] * r3[2 * 3 + 1] - r3[0 * 3 + 1] * r3[2 * 3 + 2]) / dr);  // -R_oc[0][1]
+        scal[1] = (float)res_rot;
       }
       scal[2] = N;
       scal[3] = K;

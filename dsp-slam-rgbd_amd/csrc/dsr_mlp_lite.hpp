@@ -142,6 +142,19 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
   };
   auto ldb = [&](int cb, int k32) { return *reinterpret_cast<const half8*>(B + cb * 16 * PH + k32); };
   half8 b[4];
+  // E2: the accumulators start as the bias rows, copied before the first step — holding the
+  // 16 bias registers live through step 0 instead (its C operand) made the compiler spill
+  // inside the tile loop: per-tile scratch stores whose dirty lines the weight stream then
+  // evicts to HBM (+30 MB written per launch)
+  if constexpr ((LV & 256) != 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int cb = 0; cb < 8; ++cb) {
+        acc[q][cb] = ci[q];
+        asm volatile("" : "+v"(acc[q][cb]));   // keep the copy (else folded back into the C operand)
+      }
+  }
 #pragma unroll
   for (int cb = 0; cb < 3; ++cb) b[cb] = ldb(cb, 0);
   auto step = [&](auto J, auto FIRST, int t) {
@@ -158,10 +171,9 @@ __device__ __forceinline__ void gemm_lite_x(const _Float16* Wl, const _Float16* 
       b[(cb + 3) & 3] = (cb + 3 < 8) ? ldb(cb + 3, pc) : ldb(cb - 5, pn);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        floatx4 c0 = floatx4{0.f, 0.f, 0.f, 0.f};
-        if constexpr ((LV & 256) != 0) c0 = ci[q];
-        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[j][q], b[cb & 3],
-                                                            decltype(FIRST)::value ? c0 : acc[q][cb], 0, 0, 0);
+        const floatx4 c0 = floatx4{0.f, 0.f, 0.f, 0.f};
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+            a[j][q], b[cb & 3], (decltype(FIRST)::value && (LV & 256) == 0) ? c0 : acc[q][cb], 0, 0, 0);
       }
     }
     if (PRIO) __builtin_amdgcn_s_setprio(0);

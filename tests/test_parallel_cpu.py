@@ -207,11 +207,13 @@ def test_resident_shard_world2_equals_one_process():
 
 
 @pytest.mark.timeout(600)
-def test_resident_shard_world8_equals_one_process():
+def test_resident_shard_world8_equals_one_process(monkeypatch):
     """The driver's N = 8 path on CPU: 8 gloo ranks, one 64-object job of
     equal-cost objects — LPT gives every rank 8 (BASELINE config 4's split) — each rank uploads
     and runs only its shard, one all-gather returns every record to rank 0 in input order,
     bitwise the one-process ResidentShard's."""
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        monkeypatch.setenv(k, "1")          # 8 ranks on this host's cores: one BLAS thread each
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -224,7 +226,10 @@ def test_resident_shard_world8_equals_one_process():
         assert p.exitcode == 0
     from reconstruct.parallel import ResidentShard
 
-    ref = ResidentShard(_fake_optimizer(), _objects(64, ragged=False)).run()
+    from threadpoolctl import threadpool_limits
+
+    with threadpool_limits(1):              # the ranks' BLAS summation order (one thread each)
+        ref = ResidentShard(_fake_optimizer(), _objects(64, ragged=False)).run()
     assert [len(s) for s in got["shards"]] == [8] * 8 and len(got["mine"]) == 8
     assert sorted(i for s in got["shards"] for i in s) == list(range(64))
     assert got["same"] and got["gather"] > 0.0

@@ -14,4 +14,6 @@ for lib in libdsr exp_NODIAG exp_NOOUT; do
     rc=$?; echo "pmc $lib $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 done
-tools/gpu_suite_bench.sh r4c --steps 5 --warmup 1 --no-cpu-baseline --no-config4
+timeout -k 10 300 python3 tools/proto_vres.py 4096 20 > gpurun_out/r4c_proto.json 2>&1
+echo "proto rc=$?"; cat gpurun_out/r4c_proto.json
+tools/gpu_suite_bench.sh r4c --steps 5 --warmup 1
