@@ -165,6 +165,11 @@ static int fwd_variant() {
   const char* e = getenv("DSR_FWD_VARIANT");
   return e ? atoi(e) : DSR_DEFAULT_FWD_VARIANT;
 }
+static int jac_variant();
+// the decoder variants (use_tanh, xyz_in_all) are implemented in the split-fp16 kernels only
+// (the fp32-MFMA A/B variants k_mlp_fwd / k_mlp_jac implement the shipped topology)
+#define variant_kernels_ok(dec) \
+  (!((dec)->D.xyz_all || (dec)->D.use_tanh) || (fwd_variant() == 12 && jac_variant() == 12))
 
 struct dsr_decoder {
   dsr_ctx* ctx = nullptr;
@@ -382,19 +387,25 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
                      dsr_decoder** out) {
   if (!ctx || !d || !w || !out) return fail(ctx, "null argument");
   *out = nullptr;
-  // The topology DSP-SLAM ships (deep_sdf_decoder.py with dims=[512]*8, latent_in=[4],
-  // weight_norm, no xyz_in_all, no use_tanh) at CodeLength 64 or 32 (LocalMapping_util.cc:416-422
-  // handles both).  Anything else is rejected loudly.
+  // The DeepSDF topology DSP-SLAM ships (deep_sdf_decoder.py with dims=[512]*8, latent_in=[4],
+  // weight_norm) at CodeLength 64 or 32 (LocalMapping_util.cc:416-422 handles both), plus the
+  // module's use_tanh and xyz_in_all switches (:46-47, :65-67, :89-94; round 4).  Anything else
+  // — LayerNorm layers among them — is rejected loudly.
   if (d->code_len != 64 && d->code_len != 32) return fail(ctx, "libdsr supports code_len 64 or 32");
+  const int XA = d->xyz_in_all ? 1 : 0, H = XA ? HID - 3 : HID;   // xyz_in_all: 509 outputs
   const int L = d->code_len, l3 = HID - (L + 3);           // lin3 out: 445 / 477
-  const int od[9] = {512, 512, 512, l3, 512, 512, 512, 512, 1};
+  const int od[9] = {H, H, H, l3, H, H, H, H, 1};
   const int id[9] = {L + 3, 512, 512, 512, 512, 512, 512, 512, 512};
   if (d->n_layers != 9) return fail(ctx, "libdsr supports the 9-layer (dims=[512]*8) DeepSDF decoder only");
   for (int i = 0; i < 9; ++i)
     if (d->out_dim[i] != od[i] || d->in_dim[i] != id[i])
       return fail(ctx, "unsupported decoder layer shapes (expected DeepSDF 8x512 with latent_in=[4])");
   if (d->latent_in != 4) return fail(ctx, "latent_in must be [4]");
-  if (d->use_tanh || d->xyz_in_all) return fail(ctx, "use_tanh / xyz_in_all decoders are not supported");
+  if (d->use_tanh != 0 && d->use_tanh != 1) return fail(ctx, "use_tanh must be 0 or 1");
+  if (d->xyz_in_all != 0 && d->xyz_in_all != 1) return fail(ctx, "xyz_in_all must be 0 or 1");
+  if ((XA || d->use_tanh) && (fwd_variant() != 12 || jac_variant() != 12))
+    return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only (DSR_FWD_VARIANT / "
+                     "DSR_JAC_VARIANT 12)");
   size_t need = 0;
   std::vector<const float*> W(9), B(9);
   for (int i = 0; i < 9; ++i) {
@@ -406,7 +417,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   if (n_floats != need) return fail(ctx, "weight buffer has the wrong size");
   hipSetDevice(ctx->device);
 
-  auto Wat = [&](int l, int r, int c) { return W[l][(size_t)r * id[l] + c]; };
+  // rows beyond a layer's outputs (xyz_in_all: 509..511) are zero weights (and zero bias below)
+  auto Wat = [&](int l, int r, int c) { return r < od[l] ? W[l][(size_t)r * id[l] + c] : 0.f; };
   // Everything downstream uses the 64-D layout: a 32-D decoder's code columns 32..63 are zero
   // (its J_code entries there are exactly 0, H's code block there k3 I, its step 0: the 39-
   // parameter system of the reference, solved inside the 71 one).  lin4's input is [h3 (l3) |
@@ -561,6 +573,8 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   D.b8 = B[8][0];
   D.code_len = L;
   D.l3 = l3;
+  D.xyz_all = XA;
+  D.use_tanh = d->use_tanh ? 1 : 0;
   for (int l = 0; l < 8; ++l) {
     D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
     D.Wl_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hl16[l])) : nullptr;
@@ -741,6 +755,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   if (p->num_depth_samples < 2 || p->num_depth_samples > MAXM)
     return fail(ctx, "num_depth_samples must be in [2, 64]");
   if (p->num_iterations < 0) return fail(ctx, "num_iterations < 0");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   auto* b = new dsr_batch();
   b->ctx = ctx;
@@ -1565,6 +1580,15 @@ static constexpr float PROBE_TH = 0.01f, PROBE_FLOOR = 0.002f, PROBE_MAX_RATIO =
 
 static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec) {
   const auto t0 = std::chrono::steady_clock::now();
+  if (dec->D.xyz_all || dec->D.use_tanh) {   // the lite kernels implement the shipped topology only
+    dsr_decoder_info& I = dec->info;
+    I.code_len = dec->code_len;
+    I.lite_eligible = 0;
+    I.lite_probe_ratio = I.lite_probe_max_err = I.lite_probe_max_err_all = NAN;
+    I.probe_points = I.probe_codes = 0;
+    I.probe_ms = 0.0;
+    return 0;
+  }
   const int n = PROBE_POINTS, nc = PROBE_CODES, tot = n * nc;
   uint64_t s = 0x9E3779B97F4A7C15ull;           // fixed LCG: the probe set is part of the contract
   auto u01 = [&]() {
@@ -1750,6 +1774,7 @@ int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pt
   if (!ctx || !dec || !grid_pts || !out) return fail(ctx, "null argument");
   *out = nullptr;
   if (vol_dim < 2 || vol_dim > 512) return fail(ctx, "vol_dim must be in [2, 512]");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   auto* m = new dsr_mesher();
   m->ctx = ctx;
@@ -1801,6 +1826,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
                    int fcap, int* n_verts, int* n_faces) {
   if (!m || !code || !n_verts || !n_faces) return fail(m ? m->ctx : nullptr, "null argument");
   dsr_ctx* ctx = m->ctx;
+  if (!variant_kernels_ok(m->dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
   const DevDecoder& D = m->dec->D;
@@ -1871,6 +1897,7 @@ int dsr_mc_volume(dsr_ctx* ctx, const float* vol, int vol_dim, float level, floa
 int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts, int n,
                  float* sdf, float* jac) {
   if (!ctx || !dec || !code || (n > 0 && (!pts || !sdf))) return fail(ctx, "null argument");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
   if (n <= 0) return 0;
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
@@ -1955,6 +1982,7 @@ int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_pa
   if (!ctx || !dec || !p || !t_out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
   if (n_obj <= 0) return fail(ctx, "n_obj must be > 0");
   if (p->code_len != dec->code_len) return fail(ctx, "optimizer code_len != decoder code_len");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
   for (int o = 0; o < n_obj; ++o) {
     if (!in[o].code || (in[o].n_pts > 0 && !in[o].pts)) return fail(ctx, "null argument");
     if (in[o].n_pts < 0) return fail(ctx, "bad surface points");

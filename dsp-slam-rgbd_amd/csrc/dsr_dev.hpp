@@ -61,7 +61,20 @@ struct DevDecoder {
   // l3 >> 6, 16-row block (l3 >> 4) & 3, quad g = 3, rows r = 1..3 (l3 % 16 == 13 for both)
   int code_len;
   int l3;
+  // decoder variants of deep_sdf_decoder.py (split-fp16 kernels only; never lite-eligible):
+  // xyz_all (xyz_in_all, :46-47, :89-90): every hidden layer but lin3 has 509 outputs and every
+  // layer's input but lin0's / lin4's is [h (509) | xyz] — rows 509..511 (wave 7, block 3, quad
+  // 3, r 1..3, like lin4's) carry the point's x, y, z after the ReLU, lin8's included;
+  // use_tanh (:65-67, :93-94): tanh after lin8, before the final self.th — y = tanh(tanh(.))
+  int xyz_all;
+  int use_tanh;
 };
+
+// row of the point's xyz in the input of the layer after lin_l (l = 0..7), or -1: lin4's input
+// is [h3 | code (folded) | xyz] (row l3), with xyz_in_all every other layer's is [h | xyz] (509)
+__device__ __forceinline__ int xyz_row(const DevDecoder& D, int l) {
+  return l == 3 ? D.l3 : (D.xyz_all ? HID - 3 : -1);
+}
 
 // d sdf / d[code, xyz] slot (gin, 64-D layout: code 0..63, xyz 64..66) of lin4's input row n >= l3
 __device__ __forceinline__ int gin_slot(int n, int l3) { return n < HID - 3 ? n - l3 : CODE + (n - (HID - 3)); }

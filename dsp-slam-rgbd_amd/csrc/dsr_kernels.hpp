@@ -1318,6 +1318,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
             }
           }
         }
+        if (D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // xyz_in_all: lin1's input = h0 | xyz
         JSTAMP(7)
         fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
@@ -1351,7 +1352,10 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           }
         }
         mk[l] = bits;
-        if (l == 3 && w == (D.l3 >> 6)) xyz_rows(v, sm.xyz, lane, m, (D.l3 >> 4) & 3);   // lin4 input = h3 | xyz
+        {   // the next layer's input = h | xyz (lin4's; every layer's under xyz_in_all)
+          const int xr = xyz_row(D, l);
+          if (xr >= 0 && w == (xr >> 6)) xyz_rows(v, sm.xyz, lane, m, (xr >> 4) & 3);
+        }
         JSTAMP(2)
         fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
@@ -1372,7 +1376,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
-        epi_l7(acc, D, sm.red, w, lane, mk[7]);
+        epi_l7(acc, D, sm.red, w, lane, mk[7], sm.xyz);
       }
       __syncthreads();
       {
@@ -1380,12 +1384,18 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         if (tid < TILE) {
           float s = sm.red[tid];
           for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
-          sm.y[tid] = tanhf(s + D.b8);
+          float y = tanhf(s + D.b8);
+          if (D.use_tanh) y = tanhf(y);                 // use_tanh: lin8 -> tanh -> self.th
+          sm.y[tid] = y;
         }
       }
       __syncthreads();
     }
-    // ---- g7 = (1 - y^2) W8 (.) relu'(a7)
+    // xyz_in_all: d sdf / d xyz through the xyz rows of every layer's input (wave 7, block 3,
+    // quad 3, r 1..3 — the same lanes that own lin4's xyz rows), summed here, added to gin at lin1
+    float xg[4][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    const bool xlane = D.xyz_all && w == 7 && ((threadIdx.x & 63) >> 4) == 3;
+    // ---- g7 = (1 - y^2) W8 (.) relu'(a7)   (use_tanh: (1 - y^2)(1 - t^2), t = atanh y = tanh(lin8))
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       float m = 0.f;
@@ -1397,12 +1407,17 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         for (int cb = 0; cb < 4; ++cb) {
           const int p = 16 * cb + c;
           const float yy = sm.y[p];
-          const float dt = 1.f - yy * yy;
+          float dt = 1.f - yy * yy;
+          if (D.use_tanh) {
+            const float t = atanhf(yy);
+            dt = dt * (1.f - t * t);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float gv = ((mk[7] >> ((q * 4 + cb) * 4 + r)) & 1ull) ? dt * fetch4(w8, r) : 0.f;
             v[q][cb][r] = gv;
             m = fmaxf(m, fabsf(gv));
+            if (q == 3 && r >= 1 && xlane) xg[cb][r - 1] = dt * fetch4(w8, r);   // lin8's xyz columns
           }
         }
       }
@@ -1432,6 +1447,23 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           m = fmaxf(m, fabsf(gv));
         }(), ...);
       }(std::make_integer_sequence<int, 64>{});
+      if (xlane && l != 4) {
+        // xyz_in_all: layer l's input rows 509..511 are x, y, z — their gradient joins xg, and
+        // they carry no ReLU (zeroed, whatever the mask bit)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int r = 1; r < 4; ++r) {
+            xg[cb][r - 1] += accr(acc[3][cb], r) * usc;
+            v[3][cb][r] = 0.f;
+          }
+      }
+      if (l == 1 && xlane) {   // (lin4's xyz slots were written by these lanes at l == 4)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) sm.gin[(16 * cb + c) * GIN_PITCH + CODE + k] += xg[cb][k];
+      }
       if (l == 4 && w >= (D.l3 >> 6)) {
         // d/d[code, xyz] via the latent skip: lin3^T's input rows n >= l3 (445 at code_len 64:
         // wave 7 all, wave 6 rows 445..447) are lin4's code and xyz columns.  Their gradient

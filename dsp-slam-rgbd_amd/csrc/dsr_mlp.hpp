@@ -201,11 +201,14 @@ __device__ __forceinline__ void epi_fwd(floatx4 (&acc)[4][4], const float* __res
 }
 
 // lin7 epilogue fused with lin8 (512 -> 1): per-wave partial dot products -> red[w][p].
+// xyz_in_all: lin8's input rows 509..511 (wave 7, block 3, quad 3, r 1..3) are the point's
+// x, y, z (xyz: the tile's float4 points), not lin7 outputs — their mask bits stay the ReLU's (0)
 __device__ __forceinline__ void epi_l7(floatx4 (&acc)[4][4], const DevDecoder& D, float* red,
-                                       int w, int lane, uint64_t& mask) {
+                                       int w, int lane, uint64_t& mask, const float* xyz = nullptr) {
   const int g = lane >> 4, c = lane & 15;
   mask = 0;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool xr = D.xyz_all && xyz != nullptr && w == 7;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n0 = 64 * w + 16 * q + 4 * g;
@@ -213,10 +216,14 @@ __device__ __forceinline__ void epi_l7(floatx4 (&acc)[4][4], const DevDecoder& D
     const float4 w8 = *reinterpret_cast<const float4*>(D.W8 + n0);
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool on = xr && q == 3 && g == 3;
+      if (q == 3 && xr) p = *reinterpret_cast<const float4*>(xyz + (16 * cb + c) * 4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = relu_t(accr(acc[q][cb], r) + fetch4(bb, r));
+        float v = relu_t(accr(acc[q][cb], r) + fetch4(bb, r));
         if (relu_pass(v)) mask |= 1ull << ((q * 4 + cb) * 4 + r);
+        if (r >= 1) v = on ? (r == 1 ? p.x : (r == 2 ? p.y : p.z)) : v;
         part[cb] = __builtin_fmaf(fetch4(w8, r), v, part[cb]);
       }
     }

@@ -478,8 +478,8 @@ struct NoStamp {
 // `stamp(phase)` marks phase ends for the DSR_EXP_STAMP diagnostic build (k_mlp_fwd16)
 template <class Stamp = NoStamp>
 __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
-                                         Fwd16Shared& sm, int w, int lane, bool is_l3, uint64_t& mk,
-                                         int l3, Stamp stamp = Stamp{}) {
+                                         Fwd16Shared& sm, int w, int lane, uint64_t& mk, int xr,
+                                         Stamp stamp = Stamp{}) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
@@ -502,7 +502,9 @@ __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, cons
       }
     }
   }
-  if (is_l3 && w == (l3 >> 6)) xyz_rows(v, sm.xyz, lane, m, (l3 >> 4) & 3);
+  // the next layer's input rows xr..xr+2 <- x, y, z (xyz_row: lin4's input, or every layer's
+  // under xyz_in_all); the mask bits above are the ReLU's, taken before
+  if (xr >= 0 && w == (xr >> 6)) xyz_rows(v, sm.xyz, lane, m, (xr >> 4) & 3);
   stamp(2);
   const Scales2 sc = block_scale2(m, sm.wmax, w, lane);   // all waves done reading H
   stamp(3);
@@ -602,9 +604,12 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           }
         }
       }
+      uint64_t b0 = 0;
+      if constexpr (MSK) b0 = relu_bits(v);
+      if (D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // lin1's input = h0 | xyz
       sa = block_scale2(m, sm.wmax, w, lane);
       write_split(v, sa.of(w), sm.Hh, sm.Hl, w, lane);
-      if constexpr (MSK) mask_push(mq, relu_bits(v));
+      if constexpr (MSK) mask_push(mq, b0);
     }
     __syncthreads();
     floatx4 acc[4][4];
@@ -615,8 +620,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
       uint64_t mk;
-      sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, l == 3, mk, D.l3,
-                 stamp);
+      sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, mk,
+                 xyz_row(D, l), stamp);
       if constexpr (MSK) mask_push(mq, mk);
       stamp(7);
       __syncthreads();
@@ -635,7 +640,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
       uint64_t mask;
-      epi_l7(acc, D, sm.red, w, lane, mask);
+      epi_l7(acc, D, sm.red, w, lane, mask, sm.xyz);
       if constexpr (MSK) {
         mask_push(mq, mask);
         mask_store(mq, MA.msk, mbase, tl.count, w, lane);
@@ -651,6 +656,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         float s = sm.red[tid];
         for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
         float y = tanhf(s + D.b8);
+        if (D.use_tanh) y = tanhf(y);                  // use_tanh: lin8 -> tanh -> self.th
         stamp(10);
         // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
         // enter through the point or the code, so re-impose it here

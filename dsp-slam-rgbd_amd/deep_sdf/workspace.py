@@ -53,22 +53,28 @@ def fold_state(state_dict, specs):
 
 
 def check_topology(specs, layers):
-    """Reject decoder variants libdsr does not implement (loudly, never approximated)."""
+    """Reject decoder variants libdsr does not implement (loudly, never approximated): LayerNorm
+    layers, other dims / latent_in / CodeLength.  Implemented: use_tanh and xyz_in_all (split-fp16
+    kernels, never the lite pass), plain Linear layers (weight_norm=False without norm_layers, or
+    layers outside norm_layers: fold_state reads their ``weight``), and dropout / latent_dropout,
+    which are identities in eval mode (deep_sdf_decoder.py:78-83, :104-105)."""
     ns = specs["NetworkSpecs"]
-    if not ns.get("weight_norm", False):
-        raise NotImplementedError("LayerNorm DeepSDF decoders (weight_norm=False, "
+    # deep_sdf_decoder.py:58-63, :96-102: a LayerNorm follows lin{i} iff not weight_norm and i in
+    # norm_layers
+    if not ns.get("weight_norm", False) and any(i in (ns.get("norm_layers") or ()) for i in range(8)):
+        raise NotImplementedError("LayerNorm DeepSDF decoders (weight_norm=False with norm_layers, "
                                   "deep_sdf_decoder.py:58-63) are not supported by libdsr")
-    if ns.get("xyz_in_all"):
-        raise NotImplementedError("xyz_in_all decoders are not supported by libdsr")
-    if ns.get("use_tanh"):
-        raise NotImplementedError("use_tanh decoders are not supported by libdsr")
     if list(ns.get("latent_in", [])) != [4]:
         raise NotImplementedError("libdsr supports latent_in=[4] only")
+    if list(ns.get("dims", [512] * 8)) != [512] * 8:
+        raise NotImplementedError("libdsr supports dims=[512]*8 only")
     L = specs["CodeLength"]
     if L not in (64, 32):
         raise NotImplementedError("libdsr supports CodeLength 64 or 32")
+    # deep_sdf_decoder.py:41-47: xyz_in_all takes 3 outputs off every hidden layer but lin3
+    h = 509 if ns.get("xyz_in_all") else 512
     shapes = [W.shape for W, _ in layers]
-    want = [(512, L + 3)] + [(512, 512)] * 2 + [(509 - L, 512)] + [(512, 512)] * 4 + [(1, 512)]
+    want = [(h, L + 3)] + [(h, 512)] * 2 + [(509 - L, 512)] + [(h, 512)] * 4 + [(1, 512)]
     if shapes != want:
         raise NotImplementedError(f"unsupported decoder shapes {shapes}")
 
@@ -96,8 +102,9 @@ class Decoder:
         for i, (W, _) in enumerate(layers):
             desc.out_dim[i], desc.in_dim[i] = W.shape
         desc.latent_in = 4
-        desc.use_tanh = 0
-        desc.xyz_in_all = 0
+        ns = specs["NetworkSpecs"]
+        desc.use_tanh = 1 if ns.get("use_tanh") else 0          # deep_sdf_decoder.py:65-67, :93-94
+        desc.xyz_in_all = 1 if ns.get("xyz_in_all") else 0      # :46-47, :89-90
         flat = np.concatenate([np.concatenate([W.reshape(-1), b.reshape(-1)]) for W, b in layers])
         self._flat = np.ascontiguousarray(flat, np.float32)
         h = C.c_void_p()

@@ -141,16 +141,11 @@ def fold_weight_norm_np(state, specs=DEFAULT_SPECS):
     return layers
 
 
-def _forward_f64(layers, inp, latent_in=(4,)):
-    x = inp
-    n = len(layers)
-    for i, (W, b) in enumerate(layers):
-        if i in latent_in:
-            x = np.concatenate([x, inp], axis=-1)
-        x = x @ W.T.astype(np.float64) + b
-        if i < n - 1:
-            x = np.maximum(x, 0.0)
-    return x[..., 0]
+def _forward_f64(layers, inp, latent_in=(4,), xyz_in_all=False):
+    """Pre-tanh output (deep_sdf_decoder.py:75-103: latent skip, xyz_in_all concat, ReLU)."""
+    x = _features_f64(layers, inp, latent_in, xyz_in_all)
+    W, b = layers[-1]
+    return (x @ W.T.astype(np.float64) + b)[..., 0]
 
 
 def calibrate_last_bias(state, specs=DEFAULT_SPECS, seed=99, n=4096, radius=0.5):
@@ -161,18 +156,27 @@ def calibrate_last_bias(state, specs=DEFAULT_SPECS, seed=99, n=4096, radius=0.5)
     L = specs["CodeLength"]
     inp = np.concatenate([np.zeros((n, L)), p], axis=1)
     layers = fold_weight_norm_np(state, specs)
-    pre = _forward_f64(layers, inp, tuple(specs["NetworkSpecs"].get("latent_in", ())))
+    ns = specs["NetworkSpecs"]
+    pre = _forward_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")))
     last = f"module.lin{len(layers) - 1}.bias"
     state[last] = (state[last].astype(np.float64) - np.median(pre)).astype(np.float32)
     return state
 
 
-def _features_f64(layers, inp, latent_in=(4,)):
+def _features_f64(layers, inp, latent_in=(4,), xyz_in_all=False):
+    """The last layer's input: hidden features (+ xyz under xyz_in_all)."""
     x = inp
+    n = len(layers)
     for i, (W, b) in enumerate(layers[:-1]):
         if i in latent_in:
             x = np.concatenate([x, inp], axis=-1)
+        elif i != 0 and xyz_in_all:
+            x = np.concatenate([x, inp[..., -3:]], axis=-1)
         x = np.maximum(x @ W.T.astype(np.float64) + b, 0.0)
+    if n - 1 in latent_in:
+        x = np.concatenate([x, inp], axis=-1)
+    elif xyz_in_all:
+        x = np.concatenate([x, inp[..., -3:]], axis=-1)
     return x
 
 
@@ -187,7 +191,8 @@ def fit_last_layer_to_sphere(state, specs=DEFAULT_SPECS, seed=5, n=12000, radius
     L = specs["CodeLength"]
     inp = np.concatenate([np.zeros((n, L)), x], axis=1)
     layers = fold_weight_norm_np(state, specs)
-    H = _features_f64(layers, inp, tuple(specs["NetworkSpecs"].get("latent_in", ())))
+    ns = specs["NetworkSpecs"]
+    H = _features_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")))
     A = np.concatenate([H, np.ones((n, 1))], axis=1)
     tgt = np.linalg.norm(x, axis=1) - radius
     w = np.linalg.solve(A.T @ A + lam * np.eye(A.shape[1]), A.T @ tgt)

@@ -49,8 +49,12 @@ typedef struct {
   int out_dim[DSR_MAX_LAYERS];    /* rows of lin{i}.weight */
   int in_dim[DSR_MAX_LAYERS];     /* cols of lin{i}.weight */
   int latent_in;                  /* index of the layer that takes cat([x, input]) (4) */
-  int use_tanh;                   /* NetworkSpecs.use_tanh — must be 0 */
-  int xyz_in_all;                 /* must be 0 */
+  int use_tanh;                   /* NetworkSpecs.use_tanh: tanh after lin8, before the final tanh
+                                     (deep_sdf_decoder.py:65-67, 93-94) — 0 or 1 */
+  int xyz_in_all;                 /* NetworkSpecs.xyz_in_all (:46-47, 89-90): hidden layers but lin3 have
+                                     509 outputs, every layer input but lin0's / lin4's is [h | xyz] — 0 or 1.
+                                     Either variant runs the split-fp16 kernels and never the lite pass
+                                     (dsr_decoder_info.lite_eligible 0) */
 } dsr_decoder_desc;
 
 /* Optimizer hyper-parameters (reconstruct/optimizer.py:27-43; configs/config_*.json

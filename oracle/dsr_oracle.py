@@ -35,25 +35,28 @@ class Decoder:
     """DeepSDF MLP, eval mode (deep_sdf_decoder.py:10-110).
 
     ``layers`` are the *effective* (W, b) per ``lin{i}`` (weight-norm already
-    folded, W = v * (g / ||v||), deep_sdf_decoder.py:49-53).  Dropout is inert in
-    eval (:104-105).  Only the weight-norm topology DSP-SLAM ships is supported
-    (no LayerNorm :58-63/:96-102, no xyz_in_all :46-47/:89-90, no use_tanh
-    :65-67/:93-94); the final ``self.th`` tanh (:72, :107-108) is always applied.
+    folded, W = v * (g / ||v||), deep_sdf_decoder.py:49-53).  Dropout and latent
+    dropout are inert in eval (:78-83, :104-105).  Variants: ``xyz_in_all`` (every
+    layer's input but lin0's and the latent-skip layer's gets xyz appended, :89-90) and
+    ``use_tanh`` (a tanh after the last layer, before the final ``self.th``, :93-94);
+    the final ``self.th`` tanh (:72, :107-108) is always applied.  LayerNorm decoders
+    (:58-63, :96-102) are not restated.
     """
 
-    def __init__(self, layers, code_len=64, latent_in=(4,), dtype=F32):
+    def __init__(self, layers, code_len=64, latent_in=(4,), dtype=F32, xyz_in_all=False, use_tanh=False):
         self.dtype = dtype
         self.layers = [(np.asarray(W, dtype), np.asarray(b, dtype)) for W, b in layers]
         self.code_len = code_len
         self.latent_in = tuple(latent_in)
+        self.xyz_in_all = bool(xyz_in_all)
+        self.use_tanh = bool(use_tanh)
 
     @classmethod
     def from_state(cls, state, specs, dtype=F32):
         """Fold a ``module.lin{i}.weight_g/_v/bias`` state dict (workspace.py:214-218)."""
         ns = specs["NetworkSpecs"]
-        if not ns.get("weight_norm") or ns.get("xyz_in_all") or ns.get("use_tanh") \
-                or ns.get("latent_dropout"):
-            raise ValueError("unsupported DeepSDF topology for the oracle")
+        if not ns.get("weight_norm") and any(i in (ns.get("norm_layers") or ()) for i in range(8)):
+            raise ValueError("LayerNorm DeepSDF decoders are not restated by the oracle")
         layers = []
         i = 0
         while f"module.lin{i}.bias" in state:
@@ -67,35 +70,47 @@ class Decoder:
                 W = np.asarray(state[name + ".weight"], np.float32)
             layers.append((W, np.asarray(state[name + ".bias"], np.float32)))
             i += 1
-        return cls(layers, specs["CodeLength"], ns.get("latent_in", ()), dtype)
+        return cls(layers, specs["CodeLength"], ns.get("latent_in", ()), dtype,
+                   bool(ns.get("xyz_in_all")), bool(ns.get("use_tanh")))
 
-    def forward(self, inp, keep_masks=False):
+    def forward(self, inp, keep_masks=False, keep_pre=False):
         """inp (n, L+3) -> sdf (n,).  deep_sdf_decoder.py:75-110."""
         inp = np.asarray(inp, self.dtype)
+        xyz = inp[..., -3:]
         x = inp
         masks = []
         n_layers = len(self.layers)
         for i, (W, b) in enumerate(self.layers):
             if i in self.latent_in:
                 x = np.concatenate([x, inp], axis=-1)          # :87-88
+            elif i != 0 and self.xyz_in_all:
+                x = np.concatenate([x, xyz], axis=-1)          # :89-90
             x = x @ W.T + b                                    # :91
+            if i == n_layers - 1 and self.use_tanh:
+                x = np.tanh(x)                                 # :93-94
             if i < n_layers - 1:
                 m = x > 0
                 x = np.where(m, x, self.dtype(0))              # :103 ReLU
                 if keep_masks:
                     masks.append(m)
-        y = np.tanh(x[..., 0])                                 # :107-108 self.th
+        t = x[..., 0]
+        y = np.tanh(t)                                         # :107-108 self.th
+        if keep_pre:
+            return y, masks, t
         return (y, masks) if keep_masks else y
 
     def forward_jac(self, inp):
         """(y, dy/dinp) — what ``get_batch_sdf_jacobian`` (loss_utils.py:82-113) gets
         from autograd, restated as the analytic chain rule:
-        tanh' = 1-y^2, ReLU' = [out>0], Linear' = W^T, latent-skip split at layer 4."""
+        tanh' = 1-y^2 (use_tanh: times 1-t^2 of the inner tanh), ReLU' = [out>0],
+        Linear' = W^T, latent-skip split at layer 4, xyz_in_all columns to d/dxyz."""
         inp = np.asarray(inp, self.dtype)
-        y, masks = self.forward(inp, keep_masks=True)
+        y, masks, t = self.forward(inp, keep_masks=True, keep_pre=True)
         n_layers = len(self.layers)
         L3 = inp.shape[-1]
         g = (self.dtype(1) - y * y)[:, None]                   # d tanh
+        if self.use_tanh:
+            g = g * (self.dtype(1) - t * t)[:, None]           # d tanh of the use_tanh layer
         grad_in = np.zeros_like(inp)
         for i in range(n_layers - 1, -1, -1):
             W, _ = self.layers[i]
@@ -103,6 +118,9 @@ class Decoder:
             if i in self.latent_in:
                 grad_in = grad_in + g[:, -L3:]
                 g = g[:, :-L3]
+            elif i != 0 and self.xyz_in_all:
+                grad_in[:, -3:] = grad_in[:, -3:] + g[:, -3:]
+                g = g[:, :-3]
             if i > 0:
                 g = np.where(masks[i - 1], g, self.dtype(0))
         grad_in = g + grad_in                                  # layer-0 path + skip path

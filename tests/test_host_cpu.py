@@ -256,13 +256,14 @@ def test_grid_decode_order_matches_reference_f9(oracle_dec):
 
 @pytest.mark.parametrize("change,what", [
     ({"weight_norm": False}, "LayerNorm"),
-    ({"xyz_in_all": True}, "xyz_in_all"),
-    ({"use_tanh": True}, "use_tanh"),
+    ({"xyz_in_all": True}, "shapes"),          # implemented, but these are 8x512 lin shapes
+    ({"dims": [512] * 6}, "dims"),
     ({"latent_in": [3]}, "latent_in"),
 ])
 def test_unsupported_decoder_variants_rejected_loudly(change, what):
-    """decoder variants libdsr does not implement (deep_sdf_decoder.py:46-47,
-    58-67, 89-102) are refused before anything reaches the device, never approximated."""
+    """decoder variants libdsr does not implement (LayerNorm layers,
+    deep_sdf_decoder.py:58-63, 96-102; other dims / latent_in / CodeLength) are refused before
+    anything reaches the device, never approximated; the implemented ones pass."""
     import copy
 
     import synthetic as S
@@ -278,6 +279,15 @@ def test_unsupported_decoder_variants_rejected_loudly(change, what):
     specs["CodeLength"] = 48
     with pytest.raises(NotImplementedError, match="CodeLength"):
         check_topology(specs, layers)
+    # implemented variants: use_tanh, dropout / latent_dropout (inert in eval), plain Linear layers
+    for change in ({"use_tanh": True}, {"latent_dropout": True}, {"weight_norm": False, "norm_layers": []}):
+        ok = copy.deepcopy(S.DEFAULT_SPECS)
+        ok["NetworkSpecs"].update(change)
+        check_topology(ok, layers)
+    # xyz_in_all, with its own layer shapes (509 outputs on every hidden layer but lin3)
+    xa = copy.deepcopy(S.DEFAULT_SPECS)
+    xa["NetworkSpecs"]["xyz_in_all"] = True
+    check_topology(xa, fold_state(S.make_decoder(1234, xa), xa))
     # CodeLength 32 is supported (LocalMapping_util.cc:416-422), with its own layer shapes
     specs["CodeLength"] = 32
     with pytest.raises(NotImplementedError, match="shapes"):

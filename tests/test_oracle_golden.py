@@ -313,3 +313,59 @@ def test_oracle_code32_decoder_and_steps():
         assert tr.H.shape == (39, 39)
         assert rel(tr.H, f["it_H"][e]) <= 3e-3
         assert rel(tr.b, f["it_b"][e]) <= 1e-2
+
+
+def _variant_specs(v):
+    import copy
+
+    specs = copy.deepcopy(S.DEFAULT_SPECS)
+    ns = specs["NetworkSpecs"]
+    if v == "tanh":
+        ns["use_tanh"] = True
+    elif v == "xyz":
+        ns["xyz_in_all"] = True
+    else:
+        ns["weight_norm"] = False
+        ns["norm_layers"] = []
+    return specs
+
+
+@pytest.mark.parametrize("v", ["tanh", "xyz", "plain"])
+def test_oracle_decoder_variants(v):
+    """Golden F17 (tests/golden/make_variants.py: the REFERENCE's module with use_tanh,
+    xyz_in_all or plain Linear layers, deep_sdf_decoder.py:41-56, 89-94): the regenerated
+    decoder folds to the reference's weights bit for bit, the oracle's sdf / Jacobian match
+    get_batch_sdf_jacobian, and (use_tanh, xyz_in_all) one oracle GN step from each recorded
+    reference state matches its K, loss, H, b."""
+    import hashlib
+
+    from deep_sdf.workspace import check_topology, fold_state
+
+    f = golden("f17_variants.npz")
+    specs = _variant_specs(v)
+    layers = fold_state(S.make_decoder(1234, specs), specs)
+    check_topology(specs, layers)
+    h = hashlib.sha256()
+    for W, b in layers:
+        h.update(W.tobytes())
+        h.update(b.tobytes())
+    assert h.hexdigest() == str(f[v + "_folded_sha256"])
+    dec = O.Decoder.from_state(S.make_decoder(1234, specs), specs)
+    y, j = dec.forward_jac(np.concatenate([np.broadcast_to(f[v + "_z"], (256, 64)), f[v + "_x"]], 1))
+    assert np.abs(y - f[v + "_sdf"]).max() <= 2e-6
+    assert_jac_close(j, f[v + "_jac"], tol=2e-5)
+    assert np.abs(O.decode_sdf(dec, f[v + "_z"], f[v + "_x"]) - f[v + "_sdf_nograd"]).max() <= 2e-6
+    if v == "plain":
+        return
+    P = O.OptimParams.from_cfg(S.KITTI_OPTIM)
+    n_fg = f[v + "_obj_depth"].shape[0]
+    dobs = np.concatenate([f[v + "_obj_depth"], np.zeros(f[v + "_obj_rays"].shape[0] - n_fg)]).astype(np.float32)
+    jo = S.KITTI_OPTIM["joint_optim"]
+    for e in range(int(f[v + "_n_iters_run"])):
+        tr, _, _ = O.gn_step(dec, P, f[v + "_it_t_obj_cam"][e], f[v + "_it_z"][e], f[v + "_obj_pts"],
+                             f[v + "_obj_rays"], dobs, n_fg)
+        assert abs(tr.k - f[v + "_it_k"][e]) <= 2
+        loss_ref = jo["k1"] * f[v + "_it_render_loss"][e] + jo["k2"] * f[v + "_it_sdf_loss"][e]
+        assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref)
+        assert rel(tr.H, f[v + "_it_H"][e]) <= 3e-3
+        assert rel(tr.b, f[v + "_it_b"][e]) <= 1e-2
