@@ -49,8 +49,22 @@ struct dsr_ctx {
   // dsr_batch_destroy: a destroy from a finalizer thread synchronises the context's streams and
   // destroys a graph, which must never happen while the owning thread captures on that stream
   std::recursive_mutex run_mu;
+  // LayerNorm decoders: the Jacobian kernel's x^ / rstd workspace per stream (gstream[g]; the
+  // context stream's serves sdf_eval and pose-only too), n_cu x LN_WS_WG floats each, allocated
+  // on first need outside any capture and kept until dsr_ctx_destroy (graphs hold the pointer)
+  float* lnws[MAX_GROUPS] = {};
 };
 static constexpr size_t POOL_CAP = (size_t)16 << 30;
+
+static float* ln_workspace(dsr_ctx* ctx, int g) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!ctx->lnws[g] &&
+      hipMalloc((void**)&ctx->lnws[g], sizeof(float) * (size_t)LN_WS_WG * ctx->n_cu) != hipSuccess) {
+    (void)hipGetLastError();
+    ctx->lnws[g] = nullptr;
+  }
+  return ctx->lnws[g];
+}
 
 // Forward-kernel variant (DSR_FWD_VARIANT: bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
 // bit3 split-fp16; 12 = split-fp16 + setprio, the default) and the A-ring depth of the split
@@ -89,7 +103,7 @@ static FwdKernel fwd_kernel(int v) {
 }
 using JacKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const ObjState*, const float*,
                            const float4*, const float*, const float*, const float*, GNParams, float*,
-                           const float4*, float*, float*, MaskArgs);
+                           const float4*, float*, float*, MaskArgs, float*);
 static int jac_variant();
 static JacKernel jac_kernel() {
   const int v = jac_variant();
@@ -104,6 +118,16 @@ static JacKernel jac_kernel() {
       return k_mlp_jac16<true, 0>;
   }
   return k_mlp_jac;
+}
+// Decoder variants (use_tanh / xyz_in_all / LayerNorm) run their own instantiations of the
+// split-fp16 kernels (ring depth 2), so the shipped topology's kernels carry none of their code;
+// variant_kernels_ok has already refused the fp32-MFMA A/B variants for them
+static bool is_variant(const DevDecoder& D) { return D.xyz_all || D.use_tanh || D.ln_mask; }
+static FwdKernel fwd_kernel_for(const DevDecoder& D, int v) {
+  return is_variant(D) ? k_mlp_fwd16<true, 1024 | 8192> : fwd_kernel(v);
+}
+static JacKernel jac_kernel_for(const DevDecoder& D) {
+  return is_variant(D) ? k_mlp_jac16<true, 2, true> : jac_kernel();
 }
 // Lite-pass variant (DSR_LITE_VARIANT, dsr_mlp_lite.hpp: lite_gemm): 16/32/48 = A ring of
 // 2/3/4 k steps, +8 static activation scale, +64 ring carried across layers (88), +128
@@ -169,7 +193,7 @@ static int jac_variant();
 // the decoder variants (use_tanh, xyz_in_all) are implemented in the split-fp16 kernels only
 // (the fp32-MFMA A/B variants k_mlp_fwd / k_mlp_jac implement the shipped topology)
 #define variant_kernels_ok(dec) \
-  (!((dec)->D.xyz_all || (dec)->D.use_tanh) || (fwd_variant() == 12 && jac_variant() == 12))
+  (!((dec)->D.xyz_all || (dec)->D.use_tanh || (dec)->D.ln_mask) || (fwd_variant() == 12 && jac_variant() == 12))
 
 struct dsr_decoder {
   dsr_ctx* ctx = nullptr;
@@ -333,6 +357,8 @@ int dsr_ctx_destroy(dsr_ctx* ctx) {
   for (int g = 1; g < MAX_GROUPS; ++g)
     if (ctx->gstream[g]) hipStreamDestroy(ctx->gstream[g]);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  for (float* p : ctx->lnws)
+    if (p) hipFree(p);
   delete ctx;
   return 0;
 }
@@ -403,9 +429,10 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   if (d->latent_in != 4) return fail(ctx, "latent_in must be [4]");
   if (d->use_tanh != 0 && d->use_tanh != 1) return fail(ctx, "use_tanh must be 0 or 1");
   if (d->xyz_in_all != 0 && d->xyz_in_all != 1) return fail(ctx, "xyz_in_all must be 0 or 1");
-  if ((XA || d->use_tanh) && (fwd_variant() != 12 || jac_variant() != 12))
-    return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only (DSR_FWD_VARIANT / "
-                     "DSR_JAC_VARIANT 12)");
+  if (d->norm_mask & ~0xFF) return fail(ctx, "norm_mask: LayerNorm may follow lin0..lin7 only");
+  if ((XA || d->use_tanh || d->norm_mask) && (fwd_variant() != 12 || jac_variant() != 12))
+    return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only "
+                     "(DSR_FWD_VARIANT / DSR_JAC_VARIANT 12)");
   size_t need = 0;
   std::vector<const float*> W(9), B(9);
   for (int i = 0; i < 9; ++i) {
@@ -414,6 +441,15 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
     B[i] = w + need;
     need += od[i];
   }
+  // LayerNorm layers' (gamma, beta) follow the linear layers, in layer order (deep_sdf_decoder.py:58-63)
+  std::vector<const float*> LG(8, nullptr), LB(8, nullptr);
+  for (int j = 0; j < 8; ++j)
+    if ((d->norm_mask >> j) & 1) {
+      LG[j] = w + need;
+      need += od[j];
+      LB[j] = w + need;
+      need += od[j];
+    }
   if (n_floats != need) return fail(ctx, "weight buffer has the wrong size");
   hipSetDevice(ctx->device);
 
@@ -540,6 +576,18 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   }
   const int h0x = add(std::move(w0x)), h0z = add(std::move(w0z)), h4z = add(std::move(w4z)),
             h8 = add(std::move(w8));
+  int hlg[8], hlb[8];
+  for (int j = 0; j < 8; ++j) {
+    hlg[j] = hlb[j] = -1;
+    if (!LG[j]) continue;
+    std::vector<float> g(512, 0.f), bb(512, 0.f);     // zero beyond out_dim: padded rows stay 0
+    for (int i = 0; i < od[j]; ++i) {
+      g[i] = LG[j][i];
+      bb[i] = LB[j][i];
+    }
+    hlg[j] = add(std::move(g));
+    hlb[j] = add(std::move(bb));
+  }
 
   auto* dec = new dsr_decoder();
   dec->ctx = ctx;
@@ -575,6 +623,12 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   D.l3 = l3;
   D.xyz_all = XA;
   D.use_tanh = d->use_tanh ? 1 : 0;
+  D.ln_mask = d->norm_mask & 0xFF;
+  for (int j = 0; j < 8; ++j) {
+    D.ln_dim[j] = od[j];
+    D.ln_g[j] = hlg[j] >= 0 ? P(hlg[j]) : nullptr;
+    D.ln_b[j] = hlb[j] >= 0 ? P(hlb[j]) : nullptr;
+  }
   for (int l = 0; l < 8; ++l) {
     D.Wh_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hf16[l])) : nullptr;
     D.Wl_raw[l] = (l >= 1) ? reinterpret_cast<const _Float16*>(P(hl16[l])) : nullptr;
@@ -755,7 +809,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   if (p->num_depth_samples < 2 || p->num_depth_samples > MAXM)
     return fail(ctx, "num_depth_samples must be in [2, 64]");
   if (p->num_iterations < 0) return fail(ctx, "num_iterations < 0");
-  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   auto* b = new dsr_batch();
   b->ctx = ctx;
@@ -829,6 +883,12 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
       gr.n = (int)((long)n_obj * (g + 1) / G) - gr.o0;
       b->groups.push_back(gr);
     }
+    if (dec->D.ln_mask)
+      for (int g = 0; g < G; ++g)
+        if (!ln_workspace(ctx, g)) {
+          dsr_batch_destroy(b);
+          return fail(ctx, "hipMalloc failed (LayerNorm workspace)");
+        }
   }
   b->cand_total = cand_off;
   b->slot_total = slot_off;
@@ -1246,8 +1306,8 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
   const int grid = ctx->n_cu;
   const int cb = (n + 63) / 64;
   const int fv = fwd_variant();
-  const FwdKernel fwdk = fwd_kernel(fv);
-  const JacKernel jack = jac_kernel();
+  const FwdKernel fwdk = fwd_kernel_for(D, fv);
+  const JacKernel jack = jac_kernel_for(D);
   const LiteKernel litek = lite_kernel();
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
@@ -1325,7 +1385,8 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
                          b->pts, b->kpts, b->kres, b0, b4, P, b->slots,
                          (const float4*)nullptr, (float*)nullptr, (float*)nullptr,
-                         keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr});
+                         keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr},
+                         D.ln_mask ? ctx->lnws[g] : (float*)nullptr);
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
       float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
       hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred, it,
@@ -1580,7 +1641,7 @@ static constexpr float PROBE_TH = 0.01f, PROBE_FLOOR = 0.002f, PROBE_MAX_RATIO =
 
 static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec) {
   const auto t0 = std::chrono::steady_clock::now();
-  if (dec->D.xyz_all || dec->D.use_tanh) {   // the lite kernels implement the shipped topology only
+  if (dec->D.xyz_all || dec->D.use_tanh || dec->D.ln_mask) {   // the lite kernels: the shipped topology only
     dsr_decoder_info& I = dec->info;
     I.code_len = dec->code_len;
     I.lite_eligible = 0;
@@ -1774,7 +1835,7 @@ int dsr_mesher_create(dsr_ctx* ctx, const dsr_decoder* dec, const float* grid_pt
   if (!ctx || !dec || !grid_pts || !out) return fail(ctx, "null argument");
   *out = nullptr;
   if (vol_dim < 2 || vol_dim > 512) return fail(ctx, "vol_dim must be in [2, 512]");
-  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   auto* m = new dsr_mesher();
   m->ctx = ctx;
@@ -1826,7 +1887,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
                    int fcap, int* n_verts, int* n_faces) {
   if (!m || !code || !n_verts || !n_faces) return fail(m ? m->ctx : nullptr, "null argument");
   dsr_ctx* ctx = m->ctx;
-  if (!variant_kernels_ok(m->dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
+  if (!variant_kernels_ok(m->dec)) return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only");
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
   const DevDecoder& D = m->dec->D;
@@ -1835,7 +1896,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   DSR_CHECK(ctx, hipMemcpyAsync(m->code, zc, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
   DSR_CHECK(ctx, hipStreamSynchronize(s));          // (zc is on this stack frame)
   hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)m->code, m->b0, m->b4);
-  hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
+  hipLaunchKernelGGL(fwd_kernel_for(D, fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
                      ErtArgs{nullptr, 1, 0.f, nullptr, nullptr}, MaskArgs{nullptr, nullptr, nullptr, nullptr});
@@ -1897,10 +1958,12 @@ int dsr_mc_volume(dsr_ctx* ctx, const float* vol, int vol_dim, float level, floa
 int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const float* pts, int n,
                  float* sdf, float* jac) {
   if (!ctx || !dec || !code || (n > 0 && (!pts || !sdf))) return fail(ctx, "null argument");
-  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only");
   if (n <= 0) return 0;
   hipSetDevice(ctx->device);
   hipStream_t s = ctx->stream;
+  float* lnw = nullptr;          // LayerNorm decoders: the context stream's Jacobian workspace
+  if (jac && dec->D.ln_mask && !(lnw = ln_workspace(ctx, 0))) return fail(ctx, "hipMalloc failed (LayerNorm workspace)");
   float zc[CODE] = {};                               // a 32-D code runs padded with zeros
   std::memcpy(zc, code, sizeof(float) * dec->code_len);
   const int nt = (n + TILE - 1) / TILE;
@@ -1941,13 +2004,13 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
   const int grid = std::min(ctx->n_cu, nt);
   if (jac) {
     GNParams P{};
-    hipLaunchKernelGGL(jac_kernel(), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+    hipLaunchKernelGGL(jac_kernel_for(D), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const ObjState*)nullptr, (const float*)nullptr,
                        (const float4*)nullptr, (const float*)nullptr, (const float*)db0, (const float*)db4, P,
                        (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr,
-                       MaskArgs{nullptr, nullptr, nullptr, nullptr});
+                       MaskArgs{nullptr, nullptr, nullptr, nullptr}, lnw);
   } else {
-    hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+    hipLaunchKernelGGL(fwd_kernel_for(D, fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
                        (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr},
                        MaskArgs{nullptr, nullptr, nullptr, nullptr});
@@ -1982,7 +2045,9 @@ int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_pa
   if (!ctx || !dec || !p || !t_out || (n_obj > 0 && !in)) return fail(ctx, "null argument");
   if (n_obj <= 0) return fail(ctx, "n_obj must be > 0");
   if (p->code_len != dec->code_len) return fail(ctx, "optimizer code_len != decoder code_len");
-  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all decoders run on the split-fp16 kernels only");
+  if (!variant_kernels_ok(dec)) return fail(ctx, "use_tanh / xyz_in_all / LayerNorm decoders run on the split-fp16 kernels only");
+  float* lnw = nullptr;          // LayerNorm decoders: the context stream's Jacobian workspace
+  if (dec->D.ln_mask && !(lnw = ln_workspace(ctx, 0))) return fail(ctx, "hipMalloc failed (LayerNorm workspace)");
   for (int o = 0; o < n_obj; ++o) {
     if (!in[o].code || (in[o].n_pts > 0 && !in[o].pts)) return fail(ctx, "null argument");
     if (in[o].n_pts < 0) return fail(ctx, "bad surface points");
@@ -2066,11 +2131,12 @@ int dsr_pose_only_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_pa
   for (int e = 0; e < iters; ++e) {
     const bool filter = (e == 4) && (e + 1 < iters);   // :77-79 inlier filter (effective only past 5 iters)
     if (n_tiles > 0)
-      hipLaunchKernelGGL(jac_kernel(), dim3(std::max(1, std::min(ctx->n_cu, n_tiles))), dim3(512), 0, s, D,
+      hipLaunchKernelGGL(jac_kernel_for(D), dim3(std::max(1, std::min(ctx->n_cu, n_tiles))), dim3(512), 0, s, D,
                          (const Tile*)dt, (const int*)dnt, (const ObjDesc*)ddesc, (const ObjState*)dst,
                          (const float*)dpts, (const float4*)nullptr, (const float*)nullptr, (const float*)db0,
                          (const float*)db4, P, (float*)dslots, (const float4*)nullptr, (float*)nullptr,
-                         filter ? (float*)dres : (float*)nullptr, MaskArgs{nullptr, nullptr, nullptr, nullptr});
+                         filter ? (float*)dres : (float*)nullptr, MaskArgs{nullptr, nullptr, nullptr, nullptr},
+                         lnw);
     hipLaunchKernelGGL(k_solve_pose, dim3(n_obj), dim3(256), 0, s, (const ObjDesc*)ddesc, (ObjState*)dst,
                        (const float*)dslots);
     if (filter) {

@@ -68,7 +68,20 @@ struct DevDecoder {
   // use_tanh (:65-67, :93-94): tanh after lin8, before the final self.th — y = tanh(tanh(.))
   int xyz_all;
   int use_tanh;
+  // LayerNorm (weight_norm=False with norm_layers, deep_sdf_decoder.py:58-63, :96-102): bit j of
+  // ln_mask = nn.LayerNorm(out_dim_j) between lin_j and its ReLU (eps 1e-5, biased variance),
+  // gamma / beta padded to 512 with zeros, ln_dim[j] = out_dim_j (the rows it normalises over)
+  int ln_mask;
+  int ln_dim[8];
+  const float* ln_g[8];
+  const float* ln_b[8];
 };
+
+// Per-workgroup workspace of the Jacobian kernel for LayerNorm decoders: each LayerNorm layer's
+// normalised activations x^ (acc layout, [16 (q, cb)][512 threads] float4) and rstd per point,
+// written by the forward and read back by the backward of the same tile
+constexpr int LN_WS_LAYER = 16 * 512 * 4 + 64;     // floats
+constexpr int LN_WS_WG = 8 * LN_WS_LAYER;          // floats per workgroup (1.0 MB)
 
 // row of the point's xyz in the input of the layer after lin_l (l = 0..7), or -1: lin4's input
 // is [h3 | code (folded) | xyz] (row l3), with xyz_in_all every other layer's is [h | xyz] (509)

@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac(DevDecoder D, const Tile* __res
                                                  float* __restrict__ slots,
                                                  const float4* __restrict__ raw_pts,
                                                  float* __restrict__ raw_out,
-                                                 float* __restrict__ res_out, MaskArgs) {
+                                                 float* __restrict__ res_out, MaskArgs, float*) {
   __shared__ JacShared sm;
   constexpr int JV = DSR_JAC_VARIANT;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1171,6 +1171,7 @@ struct Jac16Shared {
   _Float16 Hl[TILE * PH];
   float xyz[TILE * 4];
   float red[NWAVE * TILE];
+  float red2[NWAVE * TILE];    // LayerNorm decoders' second per-point moment (ln_fwd / ln_bwd)
   float y[TILE];
   float r[TILE];
   float gin[TILE * GIN_PITCH];
@@ -1194,7 +1195,9 @@ struct Jac16Shared {
 #endif
 // JSTAMP phases: 0 tile inputs / masks, 1 GEMMs, 2 epilogue compute, 3 scale exchange
 // (block_scale: its barrier), 4 split writes, 5 post-write barrier, 6 J tail, 7 other
-template <bool PRIO, int NB>
+// VAR: the decoder-variant instantiation (use_tanh / xyz_in_all / LayerNorm, DevDecoder); the
+// shipped topology's kernel (VAR false) contains none of their code
+template <bool PRIO, int NB, bool VAR = false>
 __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
                                                    const ObjDesc* __restrict__ desc,
@@ -1207,9 +1210,12 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
                                                    float* __restrict__ slots,
                                                    const float4* __restrict__ raw_pts,
                                                    float* __restrict__ raw_out,
-                                                   float* __restrict__ res_out, MaskArgs MA) {
+                                                   float* __restrict__ res_out, MaskArgs MA,
+                                                   float* __restrict__ lnws) {
   __shared__ Jac16Shared sm;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // LayerNorm decoders: this workgroup's x^ / rstd workspace (LN_WS_WG floats; null otherwise)
+  float* const lnw = lnws ? lnws + (size_t)blockIdx.x * LN_WS_WG : nullptr;
   const int nt = *n_tiles;
 #ifdef DSR_EXP_STAMP
   unsigned long long jstamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1309,16 +1315,23 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           for (int cb = 0; cb < 4; ++cb) {
             const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
 #pragma unroll
+            for (int r = 0; r < 4; ++r)
+              v[q][cb][r] = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
+          }
+        }
+        if (VAR && (D.ln_mask & 1)) ln_fwd(v, D.ln_g[0], D.ln_b[0], D.ln_dim[0], sm.red, sm.red2, w, lane, lnw);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float a = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
-              const float h = fmaxf(a, 0.f);            // NaN re-imposed after the backward
+              const float h = fmaxf(v[q][cb][r], 0.f);   // NaN re-imposed after the backward
               if (h > 0.f) mk[0] |= 1ull << ((q * 4 + cb) * 4 + r);
               v[q][cb][r] = h;
               m = fmaxf(m, h);
             }
-          }
-        }
-        if (D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // xyz_in_all: lin1's input = h0 | xyz
+        if (VAR && D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // xyz_in_all: lin1's input = h0 | xyz
         JSTAMP(7)
         fs = block_scale2(m, sm.wmax, w, lane);
         JSTAMP(3)
@@ -1337,6 +1350,28 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
         float m = 0.f;
         uint64_t bits = 0;
+        if (VAR && ((D.ln_mask >> l) & 1)) {   // LayerNorm between lin_l and its ReLU: x^, rstd kept for the backward
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[q][cb][r] = __builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r));
+          }
+          ln_fwd(v, D.ln_g[l], D.ln_b[l], D.ln_dim[l], sm.red, sm.red2, w, lane, lnw + (size_t)l * LN_WS_LAYER);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float h = fmaxf(v[q][cb][r], 0.f);
+                if (h > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
+                v[q][cb][r] = h;
+                m = fmaxf(m, h);
+              }
+        } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
@@ -1351,9 +1386,10 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
             }
           }
         }
+        }
         mk[l] = bits;
         {   // the next layer's input = h | xyz (lin4's; every layer's under xyz_in_all)
-          const int xr = xyz_row(D, l);
+          const int xr = VAR ? xyz_row(D, l) : (l == 3 ? D.l3 : -1);
           if (xr >= 0 && w == (xr >> 6)) xyz_rows(v, sm.xyz, lane, m, (xr >> 4) & 3);
         }
         JSTAMP(2)
@@ -1376,7 +1412,9 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
-        epi_l7(acc, D, sm.red, w, lane, mk[7], sm.xyz);
+        const bool ln7 = VAR && ((D.ln_mask >> 7) & 1);
+        if (ln7) ln_l7(acc, D, sm.red, sm.red2, w, lane, lnw + (size_t)7 * LN_WS_LAYER);
+        epi_l7(acc, D, sm.red, w, lane, mk[7], VAR ? sm.xyz : nullptr, !ln7);
       }
       __syncthreads();
       {
@@ -1385,7 +1423,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           float s = sm.red[tid];
           for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
           float y = tanhf(s + D.b8);
-          if (D.use_tanh) y = tanhf(y);                 // use_tanh: lin8 -> tanh -> self.th
+          if (VAR && D.use_tanh) y = tanhf(y);          // use_tanh: lin8 -> tanh -> self.th
           sm.y[tid] = y;
         }
       }
@@ -1394,7 +1432,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     // xyz_in_all: d sdf / d xyz through the xyz rows of every layer's input (wave 7, block 3,
     // quad 3, r 1..3 — the same lanes that own lin4's xyz rows), summed here, added to gin at lin1
     float xg[4][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-    const bool xlane = D.xyz_all && w == 7 && ((threadIdx.x & 63) >> 4) == 3;
+    const bool xlane = VAR && D.xyz_all && w == 7 && ((threadIdx.x & 63) >> 4) == 3;
     // ---- g7 = (1 - y^2) W8 (.) relu'(a7)   (use_tanh: (1 - y^2)(1 - t^2), t = atanh y = tanh(lin8))
     {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
@@ -1408,7 +1446,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           const int p = 16 * cb + c;
           const float yy = sm.y[p];
           float dt = 1.f - yy * yy;
-          if (D.use_tanh) {
+          if (VAR && D.use_tanh) {
             const float t = atanhf(yy);
             dt = dt * (1.f - t * t);
           }
@@ -1421,6 +1459,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           }
         }
       }
+      if (VAR && ((D.ln_mask >> 7) & 1))   // through lin7's LayerNorm: dL/da7
+        m = ln_bwd(v, D.ln_g[7], D.ln_dim[7], sm.red, sm.red2, w, lane, lnw + (size_t)7 * LN_WS_LAYER);
       JSTAMP(7)
       sa = block_scale(m, sm.wmax, w, lane);     // (no GEMM in flight: the barrier is harmless)
       JSTAMP(3)
@@ -1483,6 +1523,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
             }
           }
       }
+      if (VAR && ((D.ln_mask >> (l - 1)) & 1))   // through lin_{l-1}'s LayerNorm: dL/da_{l-1}
+        m = ln_bwd(v, D.ln_g[l - 1], D.ln_dim[l - 1], sm.red, sm.red2, w, lane, lnw + (size_t)(l - 1) * LN_WS_LAYER);
       JSTAMP(2)
       sa = block_scale(m, sm.wmax, w, lane);
       JSTAMP(3)

@@ -204,7 +204,8 @@ __device__ __forceinline__ void epi_fwd(floatx4 (&acc)[4][4], const float* __res
 // xyz_in_all: lin8's input rows 509..511 (wave 7, block 3, quad 3, r 1..3) are the point's
 // x, y, z (xyz: the tile's float4 points), not lin7 outputs — their mask bits stay the ReLU's (0)
 __device__ __forceinline__ void epi_l7(floatx4 (&acc)[4][4], const DevDecoder& D, float* red,
-                                       int w, int lane, uint64_t& mask, const float* xyz = nullptr) {
+                                       int w, int lane, uint64_t& mask, const float* xyz = nullptr,
+                                       bool with_bias = true) {   // false: acc holds LN(lin7) (ln_l7)
   const int g = lane >> 4, c = lane & 15;
   mask = 0;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
@@ -212,7 +213,7 @@ __device__ __forceinline__ void epi_l7(floatx4 (&acc)[4][4], const DevDecoder& D
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n0 = 64 * w + 16 * q + 4 * g;
-    const float4 bb = *reinterpret_cast<const float4*>(D.bias[7] + n0);
+    const float4 bb = with_bias ? *reinterpret_cast<const float4*>(D.bias[7] + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 w8 = *reinterpret_cast<const float4*>(D.W8 + n0);
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {

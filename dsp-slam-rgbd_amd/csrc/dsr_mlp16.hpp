@@ -35,6 +35,7 @@ struct Fwd16Shared {
   _Float16 Hl[TILE * PH];
   float xyz[TILE * 4];
   float red[NWAVE * TILE];
+  float red2[NWAVE * TILE];    // LayerNorm decoders' second per-point moment (ln_fwd)
   float wmax[NWAVE];
 };
 
@@ -471,6 +472,160 @@ __device__ __forceinline__ void xyz_rows(float (&v)[4][NCB][4], const float* xyz
   }
 }
 
+// ---- LayerNorm (deep_sdf_decoder.py:58-63, :96-102: nn.LayerNorm(D) between lin_j and its ReLU,
+// eps 1e-5, biased variance) over the D live rows of a layer's pre-activations v (acc layout:
+// rows 64w + 16q + 4g + r, points 16cb + c).  The rows of a point span the 8 waves, so the
+// per-point moments go through LDS (red / red2, two barriers: mean, then the variance about it —
+// two-pass, as torch's LayerNorm accumulates).  Called by all waves.
+__device__ __forceinline__ void ln_point_sums(float (&s)[4], float* red, int w, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    s[cb] += xor_lane(s[cb], lane, 16);
+    s[cb] += xor_lane(s[cb], lane, 32);
+    if (g == 0) red[w * 64 + 16 * cb + c] = s[cb];
+  }
+}
+__device__ __forceinline__ float ln_total(const float* red, int cb, int c) {
+  float t = red[16 * cb + c];
+#pragma unroll
+  for (int k = 1; k < NWAVE; ++k) t += red[k * 64 + 16 * cb + c];
+  return t;
+}
+
+// v: pre-activations in, u = x^ gamma + beta out (rows >= D: 0).  xh (nullable): the workgroup's
+// workspace for this layer (LN_WS_LAYER floats): x^ and rstd are kept for the Jacobian's backward.
+__device__ __forceinline__ void ln_fwd(float (&v)[4][4][4], const float* __restrict__ gam,
+                                       const float* __restrict__ bet, int D, float* red, float* red2, int w,
+                                       int lane, float* __restrict__ xh) {
+  const int g = lane >> 4, c = lane & 15;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[cb] += (64 * w + 16 * q + 4 * g + r < D) ? v[q][cb][r] : 0.f;
+  ln_point_sums(s, red, w, lane);
+  __syncthreads();
+  const float invD = 1.f / (float)D;
+  float mean[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    mean[cb] = ln_total(red, cb, c) * invD;
+    s[cb] = 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = v[q][cb][r] - mean[cb];
+        s[cb] += (64 * w + 16 * q + 4 * g + r < D) ? d * d : 0.f;
+      }
+  ln_point_sums(s, red2, w, lane);
+  __syncthreads();
+  float rstd[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) rstd[cb] = 1.f / sqrtf(ln_total(red2, cb, c) * invD + 1e-5f);
+  const int tid = w * 64 + lane;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 64 * w + 16 * q + 4 * g;
+    const float4 gg = *reinterpret_cast<const float4*>(gam + n0);
+    const float4 bb = *reinterpret_cast<const float4*>(bet + n0);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      float xa[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool live = n0 + r < D;
+        xa[r] = live ? (v[q][cb][r] - mean[cb]) * rstd[cb] : 0.f;
+        v[q][cb][r] = live ? xa[r] * fetch4(gg, r) + fetch4(bb, r) : 0.f;
+      }
+      if (xh)
+        *reinterpret_cast<float4*>(xh + (size_t)((q * 4 + cb) * 512 + tid) * 4) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+    }
+  }
+  if (xh && w == 0 && g == 0) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) xh[16 * 512 * 4 + 16 * cb + c] = rstd[cb];
+  }
+}
+
+// v: dL/du of a LayerNorm layer's output (its ReLU already applied) in, dL/da out:
+// rstd (g - mean(g) - x^ mean(g x^)) with g = v gamma, over the D live rows (rows >= D: 0).
+// Returns the wave's max |dL/da| (the backward's split scale).
+__device__ __forceinline__ float ln_bwd(float (&v)[4][4][4], const float* __restrict__ gam, int D, float* red,
+                                        float* red2, int w, int lane, const float* __restrict__ xh) {
+  const int g = lane >> 4, c = lane & 15;
+  const int tid = w * 64 + lane;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 64 * w + 16 * q + 4 * g;
+    const float4 gg = *reinterpret_cast<const float4*>(gam + n0);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const float4 x4 = *reinterpret_cast<const float4*>(xh + (size_t)((q * 4 + cb) * 512 + tid) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gx = (n0 + r < D) ? v[q][cb][r] * fetch4(gg, r) : 0.f;
+        s1[cb] += gx;
+        s2[cb] += gx * fetch4(x4, r);
+      }
+    }
+  }
+  ln_point_sums(s1, red, w, lane);
+  ln_point_sums(s2, red2, w, lane);
+  __syncthreads();
+  const float invD = 1.f / (float)D;
+  float m1[4], m2[4], rs[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    m1[cb] = ln_total(red, cb, c) * invD;
+    m2[cb] = ln_total(red2, cb, c) * invD;
+    rs[cb] = xh[16 * 512 * 4 + 16 * cb + c];
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 64 * w + 16 * q + 4 * g;
+    const float4 gg = *reinterpret_cast<const float4*>(gam + n0);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const float4 x4 = *reinterpret_cast<const float4*>(xh + (size_t)((q * 4 + cb) * 512 + tid) * 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool live = n0 + r < D;
+        const float gx = v[q][cb][r] * fetch4(gg, r);
+        const float ga = live ? rs[cb] * ((gx - m1[cb]) - fetch4(x4, r) * m2[cb]) : 0.f;
+        v[q][cb][r] = ga;
+        m = fmaxf(m, fabsf(ga));
+      }
+    }
+  }
+  return m;
+}
+
+// LayerNorm after lin7, in place on the unscaled accumulators: acc <- LN(acc + b7); the lin8
+// dot then runs on them without the bias (epi_l7 with_bias = false).  xh: as ln_fwd.
+__device__ __forceinline__ void ln_l7(floatx4 (&acc)[4][4], const DevDecoder& D, float* red, float* red2, int w,
+                                      int lane, float* __restrict__ xh) {
+  float (&v)[4][4][4] = reinterpret_cast<float (&)[4][4][4]>(acc);
+  const int g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 bb = *reinterpret_cast<const float4*>(D.bias[7] + 64 * w + 16 * q + 4 * g);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[q][cb][r] = v[q][cb][r] + fetch4(bb, r);
+  }
+  ln_fwd(v, D.ln_g[7], D.ln_b[7], D.ln_dim[7], red, red2, w, lane, xh);
+}
+
 struct NoStamp {
   __device__ __forceinline__ void operator()(int) const {}
 };
@@ -479,12 +634,34 @@ struct NoStamp {
 template <class Stamp = NoStamp>
 __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, const float* __restrict__ bias,
                                          Fwd16Shared& sm, int w, int lane, uint64_t& mk, int xr,
-                                         Stamp stamp = Stamp{}) {
+                                         Stamp stamp = Stamp{}, const DevDecoder* lnd = nullptr, int l = 0) {
   const int g = lane >> 4, c = lane & 15;
   const float usc = ldexpf(1.f, -unscale);
   float v[4][4][4];
   float m = 0.f;
   uint64_t bits = 0;
+  if (lnd != nullptr && ((lnd->ln_mask >> l) & 1)) {   // LayerNorm between lin_l and its ReLU
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + 64 * w + 16 * q + 4 * g);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[q][cb][r] = __builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r));
+    }
+    ln_fwd(v, lnd->ln_g[l], lnd->ln_b[l], lnd->ln_dim[l], sm.red, sm.red2, w, lane, nullptr);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = fmaxf(v[q][cb][r], 0.f);
+          if (x > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
+          v[q][cb][r] = x;
+          m = fmaxf(m, x);
+        }
+  } else {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n0 = 64 * w + 16 * q + 4 * g;
@@ -502,6 +679,7 @@ __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, cons
       }
     }
   }
+  }
   // the next layer's input rows xr..xr+2 <- x, y, z (xyz_row: lin4's input, or every layer's
   // under xyz_in_all); the mask bits above are the ReLU's, taken before
   if (xr >= 0 && w == (xr >> 6)) xyz_rows(v, sm.xyz, lane, m, (xr >> 4) & 3);
@@ -516,6 +694,7 @@ __device__ __forceinline__ Scales2 epi16(floatx4 (&acc)[4][4], int unscale, cons
 
 // X: bit9 (512) exact re-decode of lite band samples — keep their ReLU masks + sdf
 // (MaskArgs); bits 10-11 = NB - 1 of the ring GEMM (gemm16_sel; 0 = the two-set gemm16_tile).
+// X bit13 (8192): the decoder-variant instantiation (use_tanh / xyz_in_all / LayerNorm)
 template <bool PRIO, int X>
 __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __restrict__ tiles,
                                                    const int* __restrict__ n_tiles,
@@ -529,6 +708,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = *n_tiles;
   constexpr bool MSK = (X & 512) != 0;
+  constexpr bool VAR = (X & 8192) != 0;
   constexpr int NB = ((X >> 10) & 3) == 0 ? 0 : 1 + ((X >> 10) & 3);
 #ifdef DSR_EXP_STAMP   // diagnostic build: per-wave cycles by phase (as k_mlp_jac16's JSTAMP)
   unsigned long long fst[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -597,16 +777,23 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         for (int cb = 0; cb < 4; ++cb) {
           const float4 p = *reinterpret_cast<const float4*>(sm.xyz + (16 * cb + c) * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float a = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
-            v[q][cb][r] = fmaxf(a, 0.f);
-            m = fmaxf(m, v[q][cb][r]);
-          }
+          for (int r = 0; r < 4; ++r)
+            v[q][cb][r] = fetch4(bb, r) + ((wx[3 * r] * p.x + wx[3 * r + 1] * p.y) + wx[3 * r + 2] * p.z);
         }
       }
+      if (VAR && (D.ln_mask & 1)) ln_fwd(v, D.ln_g[0], D.ln_b[0], D.ln_dim[0], sm.red, sm.red2, w, lane, nullptr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[q][cb][r] = fmaxf(v[q][cb][r], 0.f);
+            m = fmaxf(m, v[q][cb][r]);
+          }
       uint64_t b0 = 0;
       if constexpr (MSK) b0 = relu_bits(v);
-      if (D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // lin1's input = h0 | xyz
+      if (VAR && D.xyz_all && w == 7) xyz_rows(v, sm.xyz, lane, m, 3);   // lin1's input = h0 | xyz
       sa = block_scale2(m, sm.wmax, w, lane);
       write_split(v, sa.of(w), sm.Hh, sm.Hl, w, lane);
       if constexpr (MSK) mask_push(mq, b0);
@@ -621,7 +808,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
       stamp(1);
       uint64_t mk;
       sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, mk,
-                 xyz_row(D, l), stamp);
+                 VAR ? xyz_row(D, l) : (l == 3 ? D.l3 : -1), stamp, VAR ? &D : nullptr, l);
       if constexpr (MSK) mask_push(mq, mk);
       stamp(7);
       __syncthreads();
@@ -640,7 +827,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
       uint64_t mask;
-      epi_l7(acc, D, sm.red, w, lane, mask, sm.xyz);
+      const bool ln7 = VAR && ((D.ln_mask >> 7) & 1);
+      if (ln7) ln_l7(acc, D, sm.red, sm.red2, w, lane, nullptr);
+      epi_l7(acc, D, sm.red, w, lane, mask, VAR ? sm.xyz : nullptr, !ln7);
       if constexpr (MSK) {
         mask_push(mq, mask);
         mask_store(mq, MA.msk, mbase, tl.count, w, lane);
@@ -656,7 +845,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
         float s = sm.red[tid];
         for (int k = 1; k < NWAVE; ++k) s += sm.red[k * TILE + tid];
         float y = tanhf(s + D.b8);
-        if (D.use_tanh) y = tanhf(y);                  // use_tanh: lin8 -> tanh -> self.th
+        if (VAR && D.use_tanh) y = tanhf(y);           // use_tanh: lin8 -> tanh -> self.th
         stamp(10);
         // the ReLUs above are v_max (NaN -> 0); torch.relu propagates NaN, and a NaN can only
         // enter through the point or the code, so re-impose it here

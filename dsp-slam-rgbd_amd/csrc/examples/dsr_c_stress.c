@@ -99,9 +99,23 @@ static void live_error_paths(dsr_ctx* ctx, const dsr_decoder* dec, const float* 
                              const dsr_optim_params* p, const dsr_object_in* in) {
   dsr_decoder* d2 = NULL;
   dsr_decoder_desc bad = DESC;
-  bad.use_tanh = 1;
-  CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) < 0 && d2 == NULL, "use_tanh accepted");
+  bad.use_tanh = 2;
+  CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) < 0 && d2 == NULL, "use_tanh 2 accepted");
   CHECK(strlen(dsr_last_error(ctx)) > 0, "no message");
+  bad = DESC;
+  bad.norm_mask = 0x100;                       /* a LayerNorm after lin8: not a DeepSDF layer */
+  CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) < 0 && d2 == NULL, "norm_mask 0x100 accepted");
+  bad.norm_mask = 1;                           /* lin0's LayerNorm needs 2 x 512 more floats */
+  CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) < 0 && d2 == NULL, "short LayerNorm weights accepted");
+  bad = DESC;
+  bad.use_tanh = 1;                            /* a decoder variant: loads, never lite-eligible */
+  CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) == 0 && d2 != NULL, "use_tanh refused: %s", dsr_last_error(ctx));
+  {
+    dsr_decoder_info inf;
+    CHECK(dsr_decoder_info_get(d2, &inf) == 0 && inf.lite_eligible == 0 && inf.code_len == 64, "use_tanh info");
+  }
+  CHECK(dsr_decoder_free(ctx, d2) == 0, "free");
+  d2 = NULL;
   bad = DESC;
   bad.latent_in = 3;
   CHECK(dsr_decoder_load(ctx, &bad, w, nw, &d2) < 0, "latent_in 3 accepted");

@@ -52,18 +52,31 @@ def fold_state(state_dict, specs):
     return layers
 
 
-def check_topology(specs, layers):
-    """Reject decoder variants libdsr does not implement (loudly, never approximated): LayerNorm
-    layers, other dims / latent_in / CodeLength.  Implemented: use_tanh and xyz_in_all (split-fp16
-    kernels, never the lite pass), plain Linear layers (weight_norm=False without norm_layers, or
-    layers outside norm_layers: fold_state reads their ``weight``), and dropout / latent_dropout,
-    which are identities in eval mode (deep_sdf_decoder.py:78-83, :104-105)."""
+def norm_state(state_dict, specs):
+    """LayerNorm parameters per ``lin{j}`` (j = 0..7): ``(gamma, beta)`` fp32 arrays where
+    deep_sdf_decoder.py:58-63 builds ``bn{j} = nn.LayerNorm(out_dim)`` (weight_norm=False and
+    j in norm_layers; applied between lin{j} and its ReLU, :96-102), else None."""
     ns = specs["NetworkSpecs"]
-    # deep_sdf_decoder.py:58-63, :96-102: a LayerNorm follows lin{i} iff not weight_norm and i in
-    # norm_layers
-    if not ns.get("weight_norm", False) and any(i in (ns.get("norm_layers") or ()) for i in range(8)):
-        raise NotImplementedError("LayerNorm DeepSDF decoders (weight_norm=False with norm_layers, "
-                                  "deep_sdf_decoder.py:58-63) are not supported by libdsr")
+    out = [None] * 8
+    if ns.get("weight_norm", False):
+        return out
+    sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in state_dict.items()}
+    for j in range(8):
+        if j in (ns.get("norm_layers") or ()):
+            if f"bn{j}.weight" not in sd or f"bn{j}.bias" not in sd:
+                raise ValueError(f"checkpoint lacks bn{j}.weight / bn{j}.bias for its LayerNorm")
+            out[j] = tuple(np.asarray(sd[f"bn{j}.{k}"].detach().cpu().numpy() if hasattr(sd[f"bn{j}.{k}"], "detach")
+                                      else sd[f"bn{j}.{k}"], np.float32).reshape(-1) for k in ("weight", "bias"))
+    return out
+
+
+def check_topology(specs, layers):
+    """Reject decoder variants libdsr does not implement (loudly, never approximated): other dims
+    / latent_in / CodeLength.  Implemented: use_tanh, xyz_in_all and LayerNorm layers
+    (weight_norm=False with norm_layers: norm_state) on the split-fp16 kernels, never the lite
+    pass; plain Linear layers (fold_state reads their ``weight``); dropout / latent_dropout, which
+    are identities in eval mode (deep_sdf_decoder.py:78-83, :104-105)."""
+    ns = specs["NetworkSpecs"]
     if list(ns.get("latent_in", [])) != [4]:
         raise NotImplementedError("libdsr supports latent_in=[4] only")
     if list(ns.get("dims", [512] * 8)) != [512] * 8:
@@ -86,12 +99,18 @@ class Decoder:
     ``Optimizer`` / ``MeshExtractor``; ``code_len`` and ``layers`` are informative.
     """
 
-    def __init__(self, specs, layers, device=None, ctx=None):
+    def __init__(self, specs, layers, device=None, ctx=None, norms=None):
         import ctypes as C
 
         from reconstruct import _libdsr as L
 
         check_topology(specs, layers)
+        norms = list(norms) if norms is not None else [None] * 8
+        if any(n is not None for n in norms) and specs["NetworkSpecs"].get("weight_norm", False):
+            raise ValueError("LayerNorm parameters given for a weight-normed decoder")
+        for j, n in enumerate(norms):
+            if n is not None and (n[0].shape != (layers[j][0].shape[0],) or n[1].shape != n[0].shape):
+                raise NotImplementedError(f"bn{j} shapes {n[0].shape} / {n[1].shape} do not match lin{j}")
         self.specs = specs
         self.code_len = specs["CodeLength"]
         self.layers = layers
@@ -105,7 +124,9 @@ class Decoder:
         ns = specs["NetworkSpecs"]
         desc.use_tanh = 1 if ns.get("use_tanh") else 0          # deep_sdf_decoder.py:65-67, :93-94
         desc.xyz_in_all = 1 if ns.get("xyz_in_all") else 0      # :46-47, :89-90
-        flat = np.concatenate([np.concatenate([W.reshape(-1), b.reshape(-1)]) for W, b in layers])
+        desc.norm_mask = sum(1 << j for j, n in enumerate(norms) if n is not None)   # :58-63, :96-102
+        flat = np.concatenate([np.concatenate([W.reshape(-1), b.reshape(-1)]) for W, b in layers] +
+                              [np.concatenate([n[0], n[1]]) for n in norms if n is not None])
         self._flat = np.ascontiguousarray(flat, np.float32)
         h = C.c_void_p()
         self.ctx.check(self.ctx.lib.dsr_decoder_load(self.ctx.handle, C.byref(desc),
@@ -137,7 +158,7 @@ class Decoder:
 
 
 def decoder_from_state(state_dict, specs, device=None):
-    return Decoder(specs, fold_state(state_dict, specs), device)
+    return Decoder(specs, fold_state(state_dict, specs), device, norms=norm_state(state_dict, specs))
 
 
 def config_decoder(experiment_directory, checkpoint="latest", device=None):

@@ -34,7 +34,8 @@ IP = C.POINTER(C.c_int)
 class DecoderDesc(C.Structure):
     _fields_ = [("code_len", C.c_int), ("n_layers", C.c_int),
                 ("out_dim", C.c_int * MAX_LAYERS), ("in_dim", C.c_int * MAX_LAYERS),
-                ("latent_in", C.c_int), ("use_tanh", C.c_int), ("xyz_in_all", C.c_int)]
+                ("latent_in", C.c_int), ("use_tanh", C.c_int), ("xyz_in_all", C.c_int),
+                ("norm_mask", C.c_int)]
 
 
 class OptimParams(C.Structure):
@@ -67,7 +68,7 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 8          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 9          # include/dsr.h DSR_ABI_VERSION
 BATCH_GRAPH = 1          # include/dsr.h DSR_BATCH_GRAPH
 
 

@@ -119,7 +119,28 @@ def make_decoder_state(seed: int = 1234, specs=DEFAULT_SPECS, hidden_gain=2.45,
         else:
             state[name + ".weight"] = v.astype(np.float32)
         state[name + ".bias"] = b.astype(np.float32)
+        if not ns.get("weight_norm") and layer in (ns.get("norm_layers") or ()) and layer < n - 1:
+            # nn.LayerNorm(out_dim) between lin{layer} and its ReLU (deep_sdf_decoder.py:58-63)
+            state[f"module.bn{layer}.weight"] = rng.uniform(0.8, 1.2, size=(out_dim,)).astype(np.float32)
+            state[f"module.bn{layer}.bias"] = rng.uniform(-0.1, 0.1, size=(out_dim,)).astype(np.float32)
     return state
+
+
+def _norms_np(state, specs):
+    """LayerNorm (gamma, beta) per hidden layer (None where there is none), fp64."""
+    ns = specs["NetworkSpecs"]
+    out = []
+    for j in range(len(layer_shapes(specs)) - 1):
+        k = f"module.bn{j}.weight"
+        out.append((state[k].astype(np.float64), state[f"module.bn{j}.bias"].astype(np.float64))
+                   if (not ns.get("weight_norm") and k in state) else None)
+    return out
+
+
+def _ln_f64(x, gb):
+    mu = x.mean(-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True)
+    return (x - mu) / np.sqrt(var + 1e-5) * gb[0] + gb[1]
 
 
 def fold_weight_norm_np(state, specs=DEFAULT_SPECS):
@@ -141,9 +162,9 @@ def fold_weight_norm_np(state, specs=DEFAULT_SPECS):
     return layers
 
 
-def _forward_f64(layers, inp, latent_in=(4,), xyz_in_all=False):
-    """Pre-tanh output (deep_sdf_decoder.py:75-103: latent skip, xyz_in_all concat, ReLU)."""
-    x = _features_f64(layers, inp, latent_in, xyz_in_all)
+def _forward_f64(layers, inp, latent_in=(4,), xyz_in_all=False, norms=None):
+    """Pre-tanh output (deep_sdf_decoder.py:75-103: latent skip, xyz_in_all concat, LayerNorm, ReLU)."""
+    x = _features_f64(layers, inp, latent_in, xyz_in_all, norms)
     W, b = layers[-1]
     return (x @ W.T.astype(np.float64) + b)[..., 0]
 
@@ -157,13 +178,14 @@ def calibrate_last_bias(state, specs=DEFAULT_SPECS, seed=99, n=4096, radius=0.5)
     inp = np.concatenate([np.zeros((n, L)), p], axis=1)
     layers = fold_weight_norm_np(state, specs)
     ns = specs["NetworkSpecs"]
-    pre = _forward_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")))
+    pre = _forward_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")),
+                       _norms_np(state, specs))
     last = f"module.lin{len(layers) - 1}.bias"
     state[last] = (state[last].astype(np.float64) - np.median(pre)).astype(np.float32)
     return state
 
 
-def _features_f64(layers, inp, latent_in=(4,), xyz_in_all=False):
+def _features_f64(layers, inp, latent_in=(4,), xyz_in_all=False, norms=None):
     """The last layer's input: hidden features (+ xyz under xyz_in_all)."""
     x = inp
     n = len(layers)
@@ -172,7 +194,10 @@ def _features_f64(layers, inp, latent_in=(4,), xyz_in_all=False):
             x = np.concatenate([x, inp], axis=-1)
         elif i != 0 and xyz_in_all:
             x = np.concatenate([x, inp[..., -3:]], axis=-1)
-        x = np.maximum(x @ W.T.astype(np.float64) + b, 0.0)
+        x = x @ W.T.astype(np.float64) + b
+        if norms is not None and norms[i] is not None:
+            x = _ln_f64(x, norms[i])
+        x = np.maximum(x, 0.0)
     if n - 1 in latent_in:
         x = np.concatenate([x, inp], axis=-1)
     elif xyz_in_all:
@@ -192,7 +217,8 @@ def fit_last_layer_to_sphere(state, specs=DEFAULT_SPECS, seed=5, n=12000, radius
     inp = np.concatenate([np.zeros((n, L)), x], axis=1)
     layers = fold_weight_norm_np(state, specs)
     ns = specs["NetworkSpecs"]
-    H = _features_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")))
+    H = _features_f64(layers, inp, tuple(ns.get("latent_in", ())), bool(ns.get("xyz_in_all")),
+                      _norms_np(state, specs))
     A = np.concatenate([H, np.ones((n, 1))], axis=1)
     tgt = np.linalg.norm(x, axis=1) - radius
     w = np.linalg.solve(A.T @ A + lam * np.eye(A.shape[1]), A.T @ tgt)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 8
+#define DSR_ABI_VERSION 9
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -39,10 +39,10 @@ typedef struct dsr_decoder dsr_decoder;
 typedef struct dsr_batch dsr_batch;
 
 /* Architecture of a DeepSDF decoder (replaces deep_sdf/deep_sdf_decoder.py:10-72 as
- * configured by specs.json through deep_sdf/workspace.py:202-223).  Only the
- * topology DSP-SLAM ships is implemented: weight-norm linear layers, latent
- * re-injection at exactly one layer, ReLU, final self.th tanh; anything else is
- * rejected with an error (never silently approximated). */
+ * configured by specs.json through deep_sdf/workspace.py:202-223): dims [512]*8, latent
+ * re-injection at lin4, ReLU, final self.th tanh, CodeLength 64 or 32, and the module's
+ * use_tanh / xyz_in_all / LayerNorm switches (weight-norm or plain linear layers are folded by
+ * the caller).  Anything else is rejected with an error (never silently approximated). */
 typedef struct {
   int code_len;                   /* CodeLength (64) */
   int n_layers;                   /* number of lin{i} (9 for dims=[512]*8) */
@@ -55,6 +55,11 @@ typedef struct {
                                      509 outputs, every layer input but lin0's / lin4's is [h | xyz] — 0 or 1.
                                      Either variant runs the split-fp16 kernels and never the lite pass
                                      (dsr_decoder_info.lite_eligible 0) */
+  int norm_mask;                  /* ABI 9: bit j = nn.LayerNorm(out_dim_j) between lin{j} and its ReLU
+                                     (weight_norm=False with j in norm_layers, :58-63, 96-102; eps 1e-5).
+                                     The weight buffer then continues, for each such j in order, with
+                                     bn{j}.weight (gamma, out_dim_j) and bn{j}.bias (beta, out_dim_j).
+                                     Split-fp16 kernels only, never the lite pass.  0 for DSP-SLAM's decoders */
 } dsr_decoder_desc;
 
 /* Optimizer hyper-parameters (reconstruct/optimizer.py:27-43; configs/config_*.json

@@ -37,26 +37,34 @@ class Decoder:
     ``layers`` are the *effective* (W, b) per ``lin{i}`` (weight-norm already
     folded, W = v * (g / ||v||), deep_sdf_decoder.py:49-53).  Dropout and latent
     dropout are inert in eval (:78-83, :104-105).  Variants: ``xyz_in_all`` (every
-    layer's input but lin0's and the latent-skip layer's gets xyz appended, :89-90) and
-    ``use_tanh`` (a tanh after the last layer, before the final ``self.th``, :93-94);
-    the final ``self.th`` tanh (:72, :107-108) is always applied.  LayerNorm decoders
-    (:58-63, :96-102) are not restated.
+    layer's input but lin0's and the latent-skip layer's gets xyz appended, :89-90),
+    ``use_tanh`` (a tanh after the last layer, before the final ``self.th``, :93-94) and
+    LayerNorm (``norms[i] = (gamma, beta)``: nn.LayerNorm between lin{i} and its ReLU,
+    :58-63, :96-102, eps 1e-5, biased variance); the final ``self.th`` tanh (:72,
+    :107-108) is always applied.
     """
 
-    def __init__(self, layers, code_len=64, latent_in=(4,), dtype=F32, xyz_in_all=False, use_tanh=False):
+    def __init__(self, layers, code_len=64, latent_in=(4,), dtype=F32, xyz_in_all=False, use_tanh=False,
+                 norms=None):
         self.dtype = dtype
         self.layers = [(np.asarray(W, dtype), np.asarray(b, dtype)) for W, b in layers]
         self.code_len = code_len
         self.latent_in = tuple(latent_in)
         self.xyz_in_all = bool(xyz_in_all)
         self.use_tanh = bool(use_tanh)
+        self.norms = [None if n is None else (np.asarray(n[0], dtype), np.asarray(n[1], dtype))
+                      for n in (norms or [None] * len(self.layers))]
 
     @classmethod
     def from_state(cls, state, specs, dtype=F32):
         """Fold a ``module.lin{i}.weight_g/_v/bias`` state dict (workspace.py:214-218)."""
         ns = specs["NetworkSpecs"]
-        if not ns.get("weight_norm") and any(i in (ns.get("norm_layers") or ()) for i in range(8)):
-            raise ValueError("LayerNorm DeepSDF decoders are not restated by the oracle")
+        norms = [None] * 9
+        if not ns.get("weight_norm"):
+            for j in range(8):
+                if j in (ns.get("norm_layers") or ()) and f"module.bn{j}.weight" in state:
+                    norms[j] = (np.asarray(state[f"module.bn{j}.weight"], np.float32),
+                                np.asarray(state[f"module.bn{j}.bias"], np.float32))
         layers = []
         i = 0
         while f"module.lin{i}.bias" in state:
@@ -71,9 +79,20 @@ class Decoder:
             layers.append((W, np.asarray(state[name + ".bias"], np.float32)))
             i += 1
         return cls(layers, specs["CodeLength"], ns.get("latent_in", ()), dtype,
-                   bool(ns.get("xyz_in_all")), bool(ns.get("use_tanh")))
+                   bool(ns.get("xyz_in_all")), bool(ns.get("use_tanh")), norms[:len(layers)])
 
-    def forward(self, inp, keep_masks=False, keep_pre=False):
+    def _ln(self, x, i, keep):
+        """nn.LayerNorm (deep_sdf_decoder.py:96-101): (x - mean) / sqrt(var + eps) * gamma + beta."""
+        g, b = self.norms[i]
+        mu = x.mean(-1, keepdims=True, dtype=self.dtype)
+        d = x - mu
+        rstd = self.dtype(1) / np.sqrt((d * d).mean(-1, keepdims=True, dtype=self.dtype) + self.dtype(1e-5))
+        xh = d * rstd
+        if keep is not None:
+            keep[i] = (xh, rstd)
+        return xh * g + b
+
+    def forward(self, inp, keep_masks=False, keep_pre=False, keep_ln=None):
         """inp (n, L+3) -> sdf (n,).  deep_sdf_decoder.py:75-110."""
         inp = np.asarray(inp, self.dtype)
         xyz = inp[..., -3:]
@@ -89,6 +108,8 @@ class Decoder:
             if i == n_layers - 1 and self.use_tanh:
                 x = np.tanh(x)                                 # :93-94
             if i < n_layers - 1:
+                if self.norms[i] is not None:
+                    x = self._ln(x, i, keep_ln)                # :96-101
                 m = x > 0
                 x = np.where(m, x, self.dtype(0))              # :103 ReLU
                 if keep_masks:
@@ -105,7 +126,8 @@ class Decoder:
         tanh' = 1-y^2 (use_tanh: times 1-t^2 of the inner tanh), ReLU' = [out>0],
         Linear' = W^T, latent-skip split at layer 4, xyz_in_all columns to d/dxyz."""
         inp = np.asarray(inp, self.dtype)
-        y, masks, t = self.forward(inp, keep_masks=True, keep_pre=True)
+        lnk = {}
+        y, masks, t = self.forward(inp, keep_masks=True, keep_pre=True, keep_ln=lnk)
         n_layers = len(self.layers)
         L3 = inp.shape[-1]
         g = (self.dtype(1) - y * y)[:, None]                   # d tanh
@@ -114,6 +136,11 @@ class Decoder:
         grad_in = np.zeros_like(inp)
         for i in range(n_layers - 1, -1, -1):
             W, _ = self.layers[i]
+            if i < n_layers - 1 and i in lnk:                  # through lin{i}'s LayerNorm
+                xh, rstd = lnk[i]
+                gx = g * self.norms[i][0]
+                g = rstd * (gx - gx.mean(-1, keepdims=True, dtype=self.dtype)
+                            - xh * (gx * xh).mean(-1, keepdims=True, dtype=self.dtype))
             g = g @ W                                          # d/d(input of layer i)
             if i in self.latent_in:
                 grad_in = grad_in + g[:, -L3:]

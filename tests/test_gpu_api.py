@@ -414,16 +414,19 @@ def test_replicated_object_matches_the_original(gpu_decoder):
     and background rays are each repeated 8x (17,984 rays x 50 samples, 32,768 points) has
     the same Gauss-Newton trajectory as the original up to summation order.  Exercises the
     tile tables, ray chunks and slot reductions at 16x / 8x the metric object's sizes.
-    One iteration: pose and loss within 1e-6, code within 1e-4 (measured 1e-9 / 0 / 2.6e-6).  Ten iterations: pose and loss within
-    1e-3; the code within 0.1 of its largest entry, because the code directions the data
-    barely constrain amplify rounding over the trajectory — the reference's own 64 ulp-
-    perturbed starts (tests/golden/f4_traj_kitti0/5.npz: ens64_code) end with codes whose
-    largest deviation from the unperturbed run is, at the median member, 0.10 / 0.35 of the
-    code's largest entry."""
+    One iteration: pose and loss within 1e-6, code within 1e-4 (measured 1e-9 / 0 / 2.6e-6).
+    Ten iterations: within the reference's own reproducibility — the code directions the data
+    barely constrain amplify rounding over the trajectory, and the reference's 64 ulp-perturbed
+    starts (tests/golden/f4_traj_kitti0/5.npz: ens64_*) end, at the median member, with codes
+    0.10 / 0.35 of the code's largest entry away from the unperturbed run, losses 7.7e-3 /
+    4.3e-2 (relative) and poses 6.9e-5 / 2.9e-4 away (max 7.3e-4): pose within 1e-3, code within
+    0.35, loss within 4.3e-2.  (Round 3 held the 10-iteration run to 1e-3 / 0.1 / 1e-3; round 4's
+    fp64 rotation prior changed every KITTI step's rounding and this object's replicated run
+    then measured pose 1.1e-4, code 0.144, loss 1.1e-2 — inside the reference's envelope.)"""
     ob = S.kitti_object(3, base_seed=1000)
     n_fg = ob.depth.shape[0]
     big_rays = np.concatenate([np.tile(ob.rays[:n_fg], (8, 1)), np.tile(ob.rays[n_fg:], (8, 1))])
-    for iters, tol_t, tol_z in ((1, 1e-6, 1e-4), (10, 1e-3, 1e-1)):
+    for iters, tol_t, tol_z, tol_l in ((1, 1e-6, 1e-4, 1e-6), (10, 1e-3, 0.35, 4.3e-2)):
         opt = _opt(gpu_decoder, S.KITTI_OPTIM, iters=iters)
         base = opt.reconstruct_object(ob.t_cam_obj, ob.pts, ob.rays, ob.depth)
         big = opt.reconstruct_object(ob.t_cam_obj, np.tile(ob.pts, (16, 1)), big_rays, np.tile(ob.depth, 8))
@@ -433,7 +436,7 @@ def test_replicated_object_matches_the_original(gpu_decoder):
         d_z = np.abs(big["code"] - base["code"]).max() / max(1e-6, np.abs(base["code"]).max())
         d_l = abs(big["loss"] - base["loss"]) / abs(base["loss"])
         print(f"{iters} iterations, replicated vs original: pose {d_t:.2e} code {d_z:.2e} loss {d_l:.2e}")
-        assert d_t <= tol_t and d_z <= tol_z and d_l <= tol_t
+        assert d_t <= tol_t and d_z <= tol_z and d_l <= tol_l
 
 
 def _keyframes(n_kf, dets=4, seed0=500):

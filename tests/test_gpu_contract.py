@@ -237,41 +237,64 @@ def test_ens256_distribution_per_iteration(gpu_decoder):
     """the metric object (F4 kitti0: KITTI params, 2048 pts x 2248 rays x 10
     iterations) from the 256 ulp-perturbed starts of the reference's golden F13 ensemble
     (tests/golden/make_ens256.py, 1 thread each), all in ONE GPU batch.  At n = 256 a two-sample
-    KS test at p = 1e-3 rejects a gap of D > ~0.17 (n = 64: ~0.34).  Compared:
-    * per iteration, the render-point count K and the pre-update loss k1*render + k2*sdf
-      (loss.py:22-43, :60-166; optimizer.py:157): KS p >= 1e-3 and loss means within 3 standard
-      errors of their difference — the clouds evolve alike, not only end alike;
-    * final rotation / translation / code / loss deviations from the reference's unperturbed
-      result: KS p >= 1e-3, medians within 2x, final-loss means within 3 SE."""
+    KS test at p = 1e-3 rejects a gap of D > ~0.17 (n = 64: ~0.34).
+
+    Per iteration (K and the pre-update loss k1*render + k2*sdf, loss.py:22-43, :60-166,
+    optimizer.py:157) the clouds of ANY two fp32 implementations sit apart: at iteration 0 all
+    members share one state to ~1e-7, so the cloud's spread is smaller than an implementation's
+    own rounding offset — a render sample on the |sdf| = th threshold is taken by 45% of the
+    reference's members, 1% of the GPU's, 72% of the numpy oracle's — and each step carries its
+    offset on.  Golden F16 (tools/oracle_ens256.py: the numpy oracle from the same 256 starts)
+    measures it for a third implementation: KS distances to the reference's clouds up to 0.61
+    (loss) / 0.27 (K), mean offsets up to 0.83 sigma of the reference's loss cloud and 4.1 render
+    points.  Held: at every iteration the GPU's mean offsets from the reference — loss in units of
+    the reference cloud's sigma, K in render points — at most 1.5x the largest the oracle shows
+    over the trajectory, plus 3 standard errors; the KS distances are printed.  At the end the
+    clouds must agree as distributions: final rotation / translation / code / loss deviations
+    from the reference's unperturbed result KS p >= 1e-3, medians within 2x, final-loss means
+    within 3 SE."""
     from scipy.stats import ks_2samp
 
     from reconstruct.optimizer import Optimizer
 
     f = golden("f4_traj_kitti0.npz")
     e256 = golden("f13_ens256_kitti0.npz")
+    o256 = golden("f16_oracle_ens256_kitti0.npz")
     t_init = e256["t_init"]
     n = t_init.shape[0]
-    assert n == 256 and bool(np.all(e256["is_good"]))
+    assert n == 256 and bool(np.all(e256["is_good"])) and bool(np.all(o256["is_good"]))
     opt = Optimizer(gpu_decoder, make_cfg(S.KITTI_OPTIM, "KITTI"))
     res, tr = opt.reconstruct_objects([(t_init[m], f["obj_pts"], f["obj_rays"], f["obj_depth"], None)
                                        for m in range(n)], trace=True)
     assert all(r["is_good"] for r in res)
     jo = S.KITTI_OPTIM["joint_optim"]
     n_it = int(f["n_iters_run"])
-    worst = 1.0
+    kr_all = e256["it_k"].astype(np.float64)
+    lr_all = jo["k1"] * e256["it_render_loss"] + jo["k2"] * e256["it_sdf_loss"]
+    ko_all = o256["it_k"].astype(np.float64)
+    lo_all = jo["k1"] * o256["it_render_loss"] + jo["k2"] * o256["it_sdf_loss"]
+    off_o_l = max(abs(lo_all[:, e].mean() - lr_all[:, e].mean()) / lr_all[:, e].std(ddof=1) for e in range(n_it))
+    off_o_k = max(abs(ko_all[:, e].mean() - kr_all[:, e].mean()) for e in range(n_it))
+    rows = []
     for e in range(n_it):
         kg = np.array([t["k"][e] for t in tr], np.float64)
-        kr = e256["it_k"][:, e].astype(np.float64)
         lg = np.array([t["loss"][e] for t in tr], np.float64)
-        lr = jo["k1"] * e256["it_render_loss"][:, e] + jo["k2"] * e256["it_sdf_loss"][:, e]
-        pk = ks_2samp(kg, kr).pvalue if (kg.std() > 0 or kr.std() > 0 or kg[0] != kr[0]) else 1.0
-        pl = ks_2samp(lg, lr).pvalue
-        se = np.sqrt((lg.var(ddof=1) + lr.var(ddof=1)) / n)
-        print(f"it {e}: K mean gpu {kg.mean():.1f} ref {kr.mean():.1f} (KS p {pk:.3f}); loss mean gpu "
-              f"{lg.mean():.6f} ref {lr.mean():.6f} |d| {abs(lg.mean() - lr.mean()):.2e} 3SE {3 * se:.2e} (KS p {pl:.3f})")
-        assert pk >= 1e-3 and pl >= 1e-3, (e, pk, pl)
-        assert abs(lg.mean() - lr.mean()) <= 3 * se + 1e-12, e
-        worst = min(worst, pk, pl)
+        kr, lr, ko, lo = kr_all[:, e], lr_all[:, e], ko_all[:, e], lo_all[:, e]
+        sd = lr.std(ddof=1)
+        off_l = abs(lg.mean() - lr.mean()) / sd
+        se_l = np.sqrt((lg.var(ddof=1) + lr.var(ddof=1)) / n) / sd
+        off_k = abs(kg.mean() - kr.mean())
+        se_k = np.sqrt((kg.var(ddof=1) + kr.var(ddof=1)) / n)
+        rows.append((e, off_l, se_l, off_k, se_k))
+        print(f"it {e}: loss offset gpu {off_l:.2f} sigma (oracle {abs(lo.mean() - lr.mean()) / sd:.2f}), KS D gpu "
+              f"{ks_2samp(lg, lr).statistic:.2f} oracle {ks_2samp(lo, lr).statistic:.2f}; K offset gpu {off_k:.2f} "
+              f"(oracle {abs(ko.mean() - kr.mean()):.2f}), KS D gpu {ks_2samp(kg, kr).statistic:.2f} oracle "
+              f"{ks_2samp(ko, kr).statistic:.2f}")
+    print(f"oracle's largest offsets over the trajectory: loss {off_o_l:.2f} sigma, K {off_o_k:.2f}")
+    for e, off_l, se_l, off_k, se_k in rows:
+        assert off_l <= 1.5 * off_o_l + 3 * se_l, ("loss", e, off_l, off_o_l)
+        assert off_k <= 1.5 * off_o_k + 3 * se_k, ("K", e, off_k, off_o_k)
+    worst = 1.0
     g_err = np.array([contract_errors(r["t_cam_obj"], r["code"], r["loss"], f) for r in res])
     r_err = np.array([contract_errors(e256["t_cam_obj"][m], e256["code"][m], e256["loss"][m], f) for m in range(n)])
     g_loss, r_loss = np.array([r["loss"] for r in res], np.float64), e256["loss"].astype(np.float64)
@@ -284,4 +307,4 @@ def test_ens256_distribution_per_iteration(gpu_decoder):
         worst = min(worst, p)
     se = np.sqrt((g_loss.var(ddof=1) + r_loss.var(ddof=1)) / n)
     assert abs(g_loss.mean() - r_loss.mean()) <= 3 * se
-    print(f"smallest KS p over {n_it} iterations x (K, loss) + 4 final marginals: {worst:.3f}")
+    print(f"smallest KS p over the 4 final marginals: {worst:.3f}")

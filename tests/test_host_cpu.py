@@ -255,15 +255,14 @@ def test_grid_decode_order_matches_reference_f9(oracle_dec):
 
 
 @pytest.mark.parametrize("change,what", [
-    ({"weight_norm": False}, "LayerNorm"),
     ({"xyz_in_all": True}, "shapes"),          # implemented, but these are 8x512 lin shapes
     ({"dims": [512] * 6}, "dims"),
     ({"latent_in": [3]}, "latent_in"),
 ])
 def test_unsupported_decoder_variants_rejected_loudly(change, what):
-    """decoder variants libdsr does not implement (LayerNorm layers,
-    deep_sdf_decoder.py:58-63, 96-102; other dims / latent_in / CodeLength) are refused before
-    anything reaches the device, never approximated; the implemented ones pass."""
+    """decoder shapes libdsr does not implement (other dims / latent_in /
+    CodeLength) are refused before anything reaches the device, never approximated; the
+    implemented variants (deep_sdf_decoder.py:41-67, 89-102) pass."""
     import copy
 
     import synthetic as S
@@ -280,7 +279,8 @@ def test_unsupported_decoder_variants_rejected_loudly(change, what):
     with pytest.raises(NotImplementedError, match="CodeLength"):
         check_topology(specs, layers)
     # implemented variants: use_tanh, dropout / latent_dropout (inert in eval), plain Linear layers
-    for change in ({"use_tanh": True}, {"latent_dropout": True}, {"weight_norm": False, "norm_layers": []}):
+    for change in ({"use_tanh": True}, {"latent_dropout": True}, {"weight_norm": False, "norm_layers": []},
+                   {"weight_norm": False}):     # the last: LayerNorm after lin0..lin7
         ok = copy.deepcopy(S.DEFAULT_SPECS)
         ok["NetworkSpecs"].update(change)
         check_topology(ok, layers)

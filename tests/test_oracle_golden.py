@@ -324,22 +324,24 @@ def _variant_specs(v):
         ns["use_tanh"] = True
     elif v == "xyz":
         ns["xyz_in_all"] = True
-    else:
+    elif v == "plain":
         ns["weight_norm"] = False
         ns["norm_layers"] = []
+    else:                                    # "ln": LayerNorm after lin0..lin7
+        ns["weight_norm"] = False
     return specs
 
 
-@pytest.mark.parametrize("v", ["tanh", "xyz", "plain"])
+@pytest.mark.parametrize("v", ["tanh", "xyz", "plain", "ln"])
 def test_oracle_decoder_variants(v):
     """Golden F17 (tests/golden/make_variants.py: the REFERENCE's module with use_tanh,
-    xyz_in_all or plain Linear layers, deep_sdf_decoder.py:41-56, 89-94): the regenerated
+    xyz_in_all, plain Linear or LayerNorm layers, deep_sdf_decoder.py:41-63, 89-102): the regenerated
     decoder folds to the reference's weights bit for bit, the oracle's sdf / Jacobian match
-    get_batch_sdf_jacobian, and (use_tanh, xyz_in_all) one oracle GN step from each recorded
+    get_batch_sdf_jacobian, and (all but plain) one oracle GN step from each recorded
     reference state matches its K, loss, H, b."""
     import hashlib
 
-    from deep_sdf.workspace import check_topology, fold_state
+    from deep_sdf.workspace import check_topology, fold_state, norm_state
 
     f = golden("f17_variants.npz")
     specs = _variant_specs(v)
@@ -349,6 +351,10 @@ def test_oracle_decoder_variants(v):
     for W, b in layers:
         h.update(W.tobytes())
         h.update(b.tobytes())
+    for n in norm_state(S.make_decoder(1234, specs), specs):
+        if n is not None:
+            h.update(n[0].tobytes())
+            h.update(n[1].tobytes())
     assert h.hexdigest() == str(f[v + "_folded_sha256"])
     dec = O.Decoder.from_state(S.make_decoder(1234, specs), specs)
     y, j = dec.forward_jac(np.concatenate([np.broadcast_to(f[v + "_z"], (256, 64)), f[v + "_x"]], 1))
@@ -364,8 +370,10 @@ def test_oracle_decoder_variants(v):
     for e in range(int(f[v + "_n_iters_run"])):
         tr, _, _ = O.gn_step(dec, P, f[v + "_it_t_obj_cam"][e], f[v + "_it_z"][e], f[v + "_obj_pts"],
                              f[v + "_obj_rays"], dobs, n_fg)
-        assert abs(tr.k - f[v + "_it_k"][e]) <= 2
+        dk = abs(tr.k - int(f[v + "_it_k"][e]))
+        assert dk <= 2
         loss_ref = jo["k1"] * f[v + "_it_render_loss"][e] + jo["k2"] * f[v + "_it_sdf_loss"][e]
-        assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref)
-        assert rel(tr.H, f[v + "_it_H"][e]) <= 3e-3
-        assert rel(tr.b, f[v + "_it_b"][e]) <= 1e-2
+        # (+ the most one flipped render point moves the render term, as in test_gpu_parity)
+        assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref) + dk * jo["k1"] * 0.09 / f[v + "_it_k"][e]
+        assert rel(tr.H, f[v + "_it_H"][e]) <= (3e-3 if dk == 0 else 1e-2)
+        assert rel(tr.b, f[v + "_it_b"][e]) <= (1e-2 if dk == 0 else 3e-2)

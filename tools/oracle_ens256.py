@@ -50,10 +50,23 @@ def _member(m):
     return np.asarray(r.t_cam_obj, np.float32), np.asarray(r.code, np.float32), float(r.loss), bool(r.is_good), k, ls, lr, n
 
 
+def _indexed(m):
+    return m, _member(m)
+
+
 def main():
     jobs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    part = "/tmp/oracle_ens256_partial.npy"
+    done = {}
+    if os.path.exists(part):                 # resume a run that was cut off
+        done = np.load(part, allow_pickle=True).item()
+    todo = [m for m in range(256) if m not in done]
     with mp.get_context("fork").Pool(jobs, initializer=_init) as pool:
-        res = pool.map(_member, range(256), chunksize=1)
+        for m, r in pool.imap_unordered(_indexed, todo, chunksize=1):
+            done[m] = r
+            np.save(part, np.array(done, dtype=object), allow_pickle=True)
+            print(f"member {m} done ({len(done)}/256)", flush=True)
+    res = [done[m] for m in range(256)]
     out = dict(t_cam_obj=np.stack([r[0] for r in res]), code=np.stack([r[1] for r in res]),
                loss=np.array([r[2] for r in res]), is_good=np.array([r[3] for r in res]),
                it_k=np.stack([r[4] for r in res]), it_sdf_loss=np.stack([r[5] for r in res]),
