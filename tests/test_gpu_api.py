@@ -544,3 +544,52 @@ def test_capacity_batch_edges(gpu_decoder):
         _same([opt._result(o) for o in outs2[:2]], opt.reconstruct_objects(full[:2]))
     finally:
         lib.dsr_batch_destroy(h)
+
+
+def test_batches_released_from_another_thread(gpu_decoder):
+    """batches of async handles may be finished and destroyed on another Python
+    thread (a finalizer, a worker) while the owning thread captures and replays graphs on the
+    context's streams.  The context serialises that stream work (dsr_ctx.run_mu: launch, graph
+    capture, refill, redo, download, destroy): a keyframe stream in graph mode on the main
+    thread, one-shot batches released by a worker thread at the same time, every record bitwise
+    that of the same work run serially."""
+    import queue
+    import threading
+
+    kfs = _keyframes(12)
+    extra = [[(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in (S.redwood_object(700 + 3 * k + i)
+                                                                     for i in range(3))] for k in range(12)]
+    opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")
+    opt.keyframe_mode = "graph"
+    ref_kf = [opt.reconstruct_keyframe(d) for d in kfs]
+    ref_ex = [opt.reconstruct_objects(x) for x in extra]
+    opt.close_slots()
+    q, got, errs = queue.Queue(), {}, []
+
+    def worker():
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            k, h = item
+            try:
+                got[k] = h.wait()
+                del h                            # dsr_batch_destroy on this thread
+            except Exception as ex:             # noqa: BLE001 — reported below
+                errs.append(repr(ex))
+
+    t = threading.Thread(target=worker)
+    t.start()
+    out_kf = []
+    try:
+        for k, d in enumerate(kfs):
+            q.put((k, opt.reconstruct_objects_async(extra[k])))
+            out_kf.append(opt.reconstruct_keyframe(d))
+    finally:
+        q.put(None)
+        t.join(timeout=120)
+    assert not t.is_alive() and not errs, errs
+    for k in range(len(kfs)):
+        _same(out_kf[k], ref_kf[k])
+        _same(got[k], ref_ex[k])
+    opt.close_slots()
