@@ -583,17 +583,24 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_emit(const RenderChunk* 
 // tile tables (single workgroup)
 // ------------------------------------------------------------------------------------
 // Tile tables (one block of 1024 threads): a block-wide exclusive scan of the per-object tile
-// counts gives every object its first tile, then each thread writes its object's tiles.
+// counts gives every object its first tile; then the whole block writes the tiles, thread t
+// taking tiles t, t + 1024, ... of the chunk and finding its object by a binary search over
+// the chunk's first-tile offsets in LDS (one thread per object writing all of that object's
+// tiles was a serial loop of ~250 stores for one KITTI object's render pass, ~10 us).
 // Object order, then tile order within an object — the table the serial loop would build.
+constexpr int TILE_SCAN_THREADS = 1024;
 template <class Count, class Emit>
 __device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit emit) {
   __shared__ int wsum[16];
   __shared__ int carry;
+  __shared__ int first_s[TILE_SCAN_THREADS + 1];   // chunk-relative first tile per object, + total
+  __shared__ int n_s[TILE_SCAN_THREADS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
   if (tid == 0) carry = base;
   __syncthreads();
   for (int o0 = 0; o0 < n_obj; o0 += blockDim.x) {
     const int o = o0 + tid;
+    const int m = min((int)blockDim.x, n_obj - o0);   // objects in this chunk
     int n = 0, nt = 0;
     if (o < n_obj) count(o, n, nt);
     const int inc = wave_incl_scan(nt, lane);
@@ -605,10 +612,23 @@ __device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit 
       if (lane < nw) wsum[lane] = v;
     }
     __syncthreads();
-    const int first = carry + (wv ? wsum[wv - 1] : 0) + inc - nt;
-    for (int i = 0; i < nt; ++i) emit(first + i, o, i, n);
+    if (tid < m) {
+      first_s[tid] = (wv ? wsum[wv - 1] : 0) + inc - nt;
+      n_s[tid] = n;
+    }
+    if (tid == 0) first_s[m] = wsum[nw - 1];
     __syncthreads();
-    if (tid == 0) carry += wsum[nw - 1];
+    const int c0 = carry, ct = first_s[m];
+    for (int t = tid; t < ct; t += blockDim.x) {
+      int lo = 0, hi = m - 1;                 // last object whose first tile is <= t
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (first_s[mid] <= t) lo = mid; else hi = mid - 1;
+      }
+      emit(c0 + t, o0 + lo, t - first_s[lo], n_s[lo]);
+    }
+    __syncthreads();
+    if (tid == 0) carry += ct;
     __syncthreads();
   }
   return carry;

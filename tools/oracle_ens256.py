@@ -1,9 +1,9 @@
-"""The CPU oracle (numpy fp32) from the 256 ulp-perturbed starts of golden F13 (kitti0), per
+"""The CPU oracle (numpy fp32) from the 256 ulp-perturbed starts of golden F13 (kitti0, kitti5), per
 iteration (K, loss), against the reference's own F13 clouds — a third fp32 implementation of
 the algorithm, to size how far two correct fp32 implementations' per-iteration clouds sit apart
 (tests/test_gpu_contract.py::test_ens256_distribution_per_iteration).  CPU only:
 
-    python tools/oracle_ens256.py [jobs]    -> tests/golden/f16_oracle_ens256_kitti0.npz
+    python tools/oracle_ens256.py [jobs] [name]    -> tests/golden/f16_oracle_ens256_<name>.npz
 
 The output is the oracle's, not the reference's: it is test data for the GPU test's yardstick.
 """
@@ -25,15 +25,15 @@ import synthetic as S  # noqa: E402
 _W = {}
 
 
-def _init():
+def _init(name):
     from deep_sdf.workspace import fold_state
     from oracle import dsr_oracle as O
     from threadpoolctl import threadpool_limits
 
     threadpool_limits(1)
     g = os.path.join(REPO, "tests", "golden")
-    _W.update(O=O, f=dict(np.load(os.path.join(g, "f4_traj_kitti0.npz"), allow_pickle=False)),
-              e=dict(np.load(os.path.join(g, "f13_ens256_kitti0.npz"), allow_pickle=False)),
+    _W.update(O=O, f=dict(np.load(os.path.join(g, f"f4_traj_{name}.npz"), allow_pickle=False)),
+              e=dict(np.load(os.path.join(g, f"f13_ens256_{name}.npz"), allow_pickle=False)),
               dec=O.Decoder(fold_state(S.make_decoder(1234), S.DEFAULT_SPECS)),
               P=O.OptimParams.from_cfg(S.KITTI_OPTIM))
 
@@ -56,12 +56,13 @@ def _indexed(m):
 
 def main():
     jobs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    part = "/tmp/oracle_ens256_partial.npy"
+    name = sys.argv[2] if len(sys.argv) > 2 else "kitti0"
+    part = f"/tmp/oracle_ens256_{name}_partial.npy"
     done = {}
     if os.path.exists(part):                 # resume a run that was cut off
         done = np.load(part, allow_pickle=True).item()
     todo = [m for m in range(256) if m not in done]
-    with mp.get_context("fork").Pool(jobs, initializer=_init) as pool:
+    with mp.get_context("fork").Pool(jobs, initializer=_init, initargs=(name,)) as pool:
         for m, r in pool.imap_unordered(_indexed, todo, chunksize=1):
             done[m] = r
             np.save(part, np.array(done, dtype=object), allow_pickle=True)
@@ -71,7 +72,7 @@ def main():
                loss=np.array([r[2] for r in res]), is_good=np.array([r[3] for r in res]),
                it_k=np.stack([r[4] for r in res]), it_sdf_loss=np.stack([r[5] for r in res]),
                it_render_loss=np.stack([r[6] for r in res]), n_trace=np.array([r[7] for r in res]))
-    np.savez_compressed(os.path.join(REPO, "tests", "golden", "f16_oracle_ens256_kitti0.npz"), **out)
+    np.savez_compressed(os.path.join(REPO, "tests", "golden", f"f16_oracle_ens256_{name}.npz"), **out)
     print("done", out["is_good"].all(), np.unique(out["n_trace"]))
 
 
