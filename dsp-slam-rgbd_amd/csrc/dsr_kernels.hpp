@@ -1734,6 +1734,26 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       // and the fp32 chain det -> pow(1/3) -> divide puts ~1e-7 of noise into R_co[1][1]
       // (1% of res_rot) — in the reference as much as here; fp64 removes it
       // (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_the_reference)
+#ifdef DSR_EXP_PRIOR_FP32   // experiment build: the reference's fp32 chain (round 3's code)
+      float rco[16], rf[9], roc[9];
+      for (int i = 0; i < 16; ++i) rco[i] = S.Tco[i];
+      const float scf = powf(det3(rco), 0.33333334f);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) rf[i * 3 + j] = rco[i * 4 + j] / scf;
+      inv_small<3>(rf, roc);
+      const float res_rotf = 1.f - (-rf[1 * 3 + 1]);
+      for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
+      if (res_rotf < 1e-7f) {
+        scal[1] = 0.f;
+      } else {
+        jrot[3] = roc[2 * 3 + 1];
+        jrot[5] = -roc[0 * 3 + 1];
+        scal[1] = res_rotf;
+      }
+      if (false) {
+#else
+      {
+#endif
       double r3[9];
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) r3[i * 3 + j] = (double)S.Tco[i * 4 + j];
@@ -1754,6 +1774,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
         jrot[4] = 0.f;
         jrot[5] = (float)(-(r3[0 * 3 + 2] * r3[2 * 3 + 1] - r3[0 * 3 + 1] * r3[2 * 3 + 2]) / dr);  // -R_oc[0][1]
         scal[1] = (float)res_rot;
+      }
       }
       scal[2] = N;
       scal[3] = K;

@@ -2,6 +2,12 @@
 (build container only):
 
     DSR_ENS_JOBS=7 python tests/golden/make_ens256.py [name]      # default: kitti0
+    DSR_ENS_THREADS=8 DSR_ENS_JOBS=1 DSR_ENS_MEMBERS=64 python tests/golden/make_ens256.py [name]
+
+The second form is the reference with torch's 8-thread CPU kernels (a different reduction order
+from the 1-thread run: SURVEY.md §8(c), K-total 45,584 vs 44,668 on one object) from the first 64
+of the same starts -> tests/golden/f18_ens64_t8_<name>.npz: how far the reference's own cloud moves
+with its thread count, a second yardstick beside the numpy oracle's (F16).
 
 Each member is the reference's own ``Optimizer.reconstruct_object``
 (/root/reference/reconstruct/optimizer.py:90-205; 1 CPU thread, deterministic) on the golden
@@ -37,6 +43,7 @@ from make_ensemble import member_poses  # noqa: E402
 
 MEMBERS = int(os.environ.get("DSR_ENS_MEMBERS", "256"))
 JOBS = int(os.environ.get("DSR_ENS_JOBS", "7"))
+THREADS = int(os.environ.get("DSR_ENS_THREADS", "1"))
 _W = {}
 
 
@@ -45,7 +52,7 @@ def _member(job):
     f = _W["f"]
     ob = S.SyntheticObject(T.astype(np.float32), f["obj_pts"], f["obj_rays"], f["obj_depth"], None)
     t0 = time.time()
-    r, its = MG.run_traj(_W["ref"], _W["dec"], S.KITTI_OPTIM, "KITTI", ob, threads=1)
+    r, its = MG.run_traj(_W["ref"], _W["dec"], S.KITTI_OPTIM, "KITTI", ob, threads=THREADS)
     n = int(f["n_iters_run"])
     pad = lambda v, fill: list(v) + [fill] * (n - len(v))  # noqa: E731
     print(m, f"{time.time() - t0:.1f}s", float(r.loss), flush=True)
@@ -60,21 +67,25 @@ def main():
 
     import torch
 
-    torch.set_num_threads(1)
+    torch.set_num_threads(THREADS)
     name = ([a for a in sys.argv[1:] if not a.startswith("--")] or ["kitti0"])[0]
     _W["ref"] = refshim.load()
     _W["dec"] = refshim.build_decoder(S.make_decoder(MG.DECODER_SEED), S.DEFAULT_SPECS)
     _W["f"] = dict(np.load(os.path.join(HERE, f"f4_traj_{name}.npz"), allow_pickle=False))
     t_init = member_poses(_W["f"]["obj_t_cam_obj"], MEMBERS)
     jobs = list(enumerate(t_init))
-    with mp.get_context("fork").Pool(JOBS) as pool:
-        res = sorted(pool.map(_member, jobs, chunksize=1), key=lambda r: r[0])
+    if JOBS == 1:
+        res = [_member(j) for j in jobs]
+    else:
+        with mp.get_context("fork").Pool(JOBS) as pool:
+            res = sorted(pool.map(_member, jobs, chunksize=1), key=lambda r: r[0])
     out = {"t_init": t_init, "t_cam_obj": np.stack([r[1] for r in res]), "code": np.stack([r[2] for r in res]),
            "loss": np.array([r[3] for r in res]), "is_good": np.array([r[4] for r in res]),
            "it_k": np.array([r[5] for r in res], np.int32), "it_sdf_loss": np.array([r[6] for r in res]),
            "it_render_loss": np.array([r[7] for r in res]),
-           "torch": np.array(torch.__version__), "numpy": np.array(np.__version__), "threads": np.array(1)}
-    np.savez_compressed(os.path.join(HERE, f"f13_ens256_{name}.npz"), **out)
+           "torch": np.array(torch.__version__), "numpy": np.array(np.__version__), "threads": np.array(THREADS)}
+    fn = f"f13_ens256_{name}.npz" if THREADS == 1 else f"f18_ens{MEMBERS}_t{THREADS}_{name}.npz"
+    np.savez_compressed(os.path.join(HERE, fn), **out)
 
 
 if __name__ == "__main__":

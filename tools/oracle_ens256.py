@@ -4,6 +4,12 @@ the algorithm, to size how far two correct fp32 implementations' per-iteration c
 (tests/test_gpu_contract.py::test_ens256_distribution_per_iteration).  CPU only:
 
     python tools/oracle_ens256.py [jobs] [name]    -> tests/golden/f16_oracle_ens256_<name>.npz
+    DSR_ORACLE_FP64=1 DSR_ENS_MEMBERS=64 python tools/oracle_ens256.py [jobs] [name]
+                                                   -> tests/golden/f19_oracle64_ens64_<name>.npz
+
+The second form runs the oracle in fp64 from the first 64 of the same starts: each member's
+exact-arithmetic trajectory (to ~1e-16), the reference the per-iteration clouds of the fp32
+implementations (the reference, the GPU, the fp32 oracle) are measured against.
 
 The output is the oracle's, not the reference's: it is test data for the GPU test's yardstick.
 """
@@ -23,6 +29,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import synthetic as S  # noqa: E402
 
 _W = {}
+FP64 = os.environ.get("DSR_ORACLE_FP64", "0") == "1"
+MEMBERS = int(os.environ.get("DSR_ENS_MEMBERS", "256"))
 
 
 def _init(name):
@@ -34,7 +42,7 @@ def _init(name):
     g = os.path.join(REPO, "tests", "golden")
     _W.update(O=O, f=dict(np.load(os.path.join(g, f"f4_traj_{name}.npz"), allow_pickle=False)),
               e=dict(np.load(os.path.join(g, f"f13_ens256_{name}.npz"), allow_pickle=False)),
-              dec=O.Decoder(fold_state(S.make_decoder(1234), S.DEFAULT_SPECS)),
+              dec=O.Decoder(fold_state(S.make_decoder(1234), S.DEFAULT_SPECS), dtype=np.float64 if FP64 else np.float32),
               P=O.OptimParams.from_cfg(S.KITTI_OPTIM))
 
 
@@ -57,22 +65,24 @@ def _indexed(m):
 def main():
     jobs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     name = sys.argv[2] if len(sys.argv) > 2 else "kitti0"
-    part = f"/tmp/oracle_ens256_{name}_partial.npy"
+    tag = f"oracle64_ens{MEMBERS}" if FP64 else f"oracle_ens{MEMBERS}"
+    part = f"/tmp/{tag}_{name}_partial.npy"
     done = {}
     if os.path.exists(part):                 # resume a run that was cut off
         done = np.load(part, allow_pickle=True).item()
-    todo = [m for m in range(256) if m not in done]
+    todo = [m for m in range(MEMBERS) if m not in done]
     with mp.get_context("fork").Pool(jobs, initializer=_init, initargs=(name,)) as pool:
         for m, r in pool.imap_unordered(_indexed, todo, chunksize=1):
             done[m] = r
             np.save(part, np.array(done, dtype=object), allow_pickle=True)
-            print(f"member {m} done ({len(done)}/256)", flush=True)
-    res = [done[m] for m in range(256)]
+            print(f"member {m} done ({len(done)}/{MEMBERS})", flush=True)
+    res = [done[m] for m in range(MEMBERS)]
     out = dict(t_cam_obj=np.stack([r[0] for r in res]), code=np.stack([r[1] for r in res]),
                loss=np.array([r[2] for r in res]), is_good=np.array([r[3] for r in res]),
                it_k=np.stack([r[4] for r in res]), it_sdf_loss=np.stack([r[5] for r in res]),
                it_render_loss=np.stack([r[6] for r in res]), n_trace=np.array([r[7] for r in res]))
-    np.savez_compressed(os.path.join(REPO, "tests", "golden", f"f16_oracle_ens256_{name}.npz"), **out)
+    fn = f"f19_{tag}_{name}.npz" if FP64 else f"f16_{tag}_{name}.npz"
+    np.savez_compressed(os.path.join(REPO, "tests", "golden", fn), **out)
     print("done", out["is_good"].all(), np.unique(out["n_trace"]))
 
 
