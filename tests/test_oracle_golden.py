@@ -164,6 +164,33 @@ def test_config4_ensemble_fixture_is_consistent():
     assert lo <= float(f["loss"]) <= hi and hi - lo < 0.05 * float(f["loss"])
 
 
+@pytest.mark.parametrize("name", ["kitti0", "kitti5"])
+def test_exact_arithmetic_ensemble_fixtures_are_consistent(name):
+    """F13 / F16 / F18 / F19 (tests/golden/make_ens256.py, tools/oracle_ens256.py): the reference's
+    256-member 1-thread ensemble, the fp32 oracle's, the reference's 8-thread 64-member one and the
+    fp64 oracle's (exact arithmetic) start from the same ulp-perturbed poses (the shared
+    generator's); at iteration 0 — one state for every member — the three fp32 clouds and exact
+    arithmetic agree to fp32 rounding (loss within 2e-4 relative, K within 2 render points), and
+    every member of every cloud is good over its 10 iterations."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_ensemble import member_poses
+
+    f4 = golden(f"f4_traj_{name}.npz")
+    ref, orc, t8, ex = (golden(g) for g in (f"f13_ens256_{name}.npz", f"f16_oracle_ens256_{name}.npz",
+                                            f"f18_ens64_t8_{name}.npz", f"f19_oracle64_ens64_{name}.npz"))
+    assert np.array_equal(ref["t_init"], member_poses(f4["obj_t_cam_obj"], 256))
+    assert np.array_equal(t8["t_init"], ref["t_init"][:64]) and int(t8["threads"]) == 8
+    for g in (ref, orc, t8, ex):
+        assert bool(np.all(g["is_good"])) and (g["it_k"] >= 0).all() and g["it_k"].shape[1] == 10
+    lx = (ex["it_render_loss"] + 100.0 * ex["it_sdf_loss"])[:, 0]
+    for g in (ref, orc, t8):
+        lg = (g["it_render_loss"] + 100.0 * g["it_sdf_loss"])[:64, 0]
+        assert np.abs(lg / lx - 1.0).max() <= 2e-4
+        assert np.abs(g["it_k"][:64, 0].astype(np.int64) - ex["it_k"][:, 0]).max() <= 2
+
+
 def test_failure_semantics():
     """F6: the reference returns is_good=False, loss = previous (0. at iteration 0)."""
     f = golden("f6_fail.npz")
