@@ -1666,6 +1666,52 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict_
   red[(size_t)o * 2 * SLOT_FLOATS + SLOT_FLOATS + e] = b;
 }
 
+// Rotation prior (compute_rotation_loss_sim3, loss.py:169-192) at the pre-update pose: returns
+// res_rot (0 below 1e-7, where the reference zeroes it) and writes its Jacobian J_rot (slots 3
+// and 5; the rest zero).  Evaluated in fp64 from the fp32 inverse(T) (the reference's own
+// t_cam_obj, same getrf/getrs as optimizer.py:122): res_rot = 1 + R_co[1][1] is a cancellation
+// ~1e-5 that k4 = 1e7 multiplies into b[3:6], and the fp32 chain det -> pow(1/3) -> divide puts
+// ~1e-7 of noise into R_co[1][1] (1% of res_rot) — in the reference as much as here; fp64
+// removes it (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_the_reference).
+__device__ inline float rotation_prior(const float* Tco, float* jrot) {
+  double r3[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r3[i * 3 + j] = (double)Tco[i * 4 + j];
+  auto det = [](const double* m) {
+    return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+           m[2] * (m[3] * m[7] - m[4] * m[6]);
+  };
+  const double sc = cbrt(det(r3));
+  for (int i = 0; i < 9; ++i) r3[i] /= sc;
+  const double dr = det(r3);
+  const double res_rot = 1.0 - (-r3[1 * 3 + 1]);             // 1 - (R_co e_y).n_g
+  for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
+  if (res_rot < 1e-7) return 0.f;
+  // (R_oc n_g) x e_y = (R_oc[2][1], 0, -R_oc[0][1]), R_oc = adj(R_co) / det(R_co)
+  jrot[3] = (float)((r3[0 * 3 + 1] * r3[2 * 3 + 0] - r3[0 * 3 + 0] * r3[2 * 3 + 1]) / dr);   // R_oc[2][1]
+  jrot[5] = (float)(-(r3[0 * 3 + 2] * r3[2 * 3 + 1] - r3[0 * 3 + 1] * r3[2 * 3 + 2]) / dr);  // -R_oc[0][1]
+  return (float)res_rot;
+}
+#ifdef DSR_EXP_PRIOR_FP32
+// Experiment build only: the reference's own fp32 chain (det -> pow(1/3) -> divide -> inverse),
+// round 3's code — DESIGN.md §5 (late round 4) used it to rule the fp64 prior out as the cause
+// of kitti5's iteration-1 offset.
+__device__ inline float rotation_prior_fp32(const float* Tco, float* jrot) {
+  float rco[16], rf[9], roc[9];
+  for (int i = 0; i < 16; ++i) rco[i] = Tco[i];
+  const float sc = powf(det3(rco), 0.33333334f);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) rf[i * 3 + j] = rco[i * 4 + j] / sc;
+  inv_small<3>(rf, roc);
+  const float res_rot = 1.f - (-rf[1 * 3 + 1]);
+  for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
+  if (res_rot < 1e-7f) return 0.f;
+  jrot[3] = roc[2 * 3 + 1];
+  jrot[5] = -roc[0 * 3 + 1];
+  return res_rot;
+}
+#endif
+
 // trace_* hold [iteration][stride objects]; the pointers are pre-offset to this launch's
 // first object (object groups on concurrent streams, dsr_batch_run).
 __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDesc* __restrict__ desc,
@@ -1728,54 +1774,12 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       S.fail_reason = f;
     } else {
       scal[0] = P.k1 * ren_loss + P.k2 * sdf_loss;                 // :157
-      // rotation prior, loss.py:169-192, at the current (pre-update) pose.  Evaluated in fp64
-      // from the fp32 inverse(T) (the reference's own t_cam_obj, same getrf/getrs as :122):
-      // res_rot = 1 + R_co[1][1] is a cancellation ~1e-5 that k4 = 1e7 multiplies into b[3:6],
-      // and the fp32 chain det -> pow(1/3) -> divide puts ~1e-7 of noise into R_co[1][1]
-      // (1% of res_rot) — in the reference as much as here; fp64 removes it
-      // (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_the_reference)
-#ifdef DSR_EXP_PRIOR_FP32   // experiment build: the reference's fp32 chain (round 3's code)
-      float rco[16], rf[9], roc[9];
-      for (int i = 0; i < 16; ++i) rco[i] = S.Tco[i];
-      const float scf = powf(det3(rco), 0.33333334f);
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) rf[i * 3 + j] = rco[i * 4 + j] / scf;
-      inv_small<3>(rf, roc);
-      const float res_rotf = 1.f - (-rf[1 * 3 + 1]);
-      for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
-      if (res_rotf < 1e-7f) {
-        scal[1] = 0.f;
-      } else {
-        jrot[3] = roc[2 * 3 + 1];
-        jrot[5] = -roc[0 * 3 + 1];
-        scal[1] = res_rotf;
-      }
-      if (false) {
+      // rotation prior, loss.py:169-192, at the current (pre-update) pose (rotation_prior)
+#ifdef DSR_EXP_PRIOR_FP32
+      scal[1] = rotation_prior_fp32(S.Tco, jrot);
 #else
-      {
+      scal[1] = rotation_prior(S.Tco, jrot);
 #endif
-      double r3[9];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) r3[i * 3 + j] = (double)S.Tco[i * 4 + j];
-      auto det = [](const double* m) {
-        return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
-               m[2] * (m[3] * m[7] - m[4] * m[6]);
-      };
-      const double sc = cbrt(det(r3));
-      for (int i = 0; i < 9; ++i) r3[i] /= sc;
-      const double dr = det(r3);
-      const double res_rot = 1.0 - (-r3[1 * 3 + 1]);             // 1 - (R_co e_y).n_g
-      for (int i = 0; i < NPOSE; ++i) jrot[i] = 0.f;
-      if (res_rot < 1e-7) {
-        scal[1] = 0.f;
-      } else {
-        // (R_oc n_g) x e_y = (R_oc[2][1], 0, -R_oc[0][1]), R_oc = adj(R_co) / det(R_co)
-        jrot[3] = (float)((r3[0 * 3 + 1] * r3[2 * 3 + 0] - r3[0 * 3 + 0] * r3[2 * 3 + 1]) / dr);   // R_oc[2][1]
-        jrot[4] = 0.f;
-        jrot[5] = (float)(-(r3[0 * 3 + 2] * r3[2 * 3 + 1] - r3[0 * 3 + 1] * r3[2 * 3 + 2]) / dr);  // -R_oc[0][1]
-        scal[1] = (float)res_rot;
-      }
-      }
       scal[2] = N;
       scal[3] = K;
     }
