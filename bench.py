@@ -297,6 +297,18 @@ def keyframe_leg(dec, n_keyframes=12, objects=4):
     return out
 
 
+def device_record(device, torch):
+    """This rank's HIP device: index, PCI location and name (ranks.devices in the line)."""
+    rec = {"rank": int(os.environ.get("RANK", "0")), "host": socket.gethostname(), "hip_device": int(device),
+           "pci_bus_id": None, "pci_domain_id": None, "name": None}
+    try:
+        p = torch.cuda.get_device_properties(int(device))
+        rec.update(pci_bus_id=int(p.pci_bus_id), pci_domain_id=int(p.pci_domain_id), name=p.name)
+    except Exception:
+        pass
+    return rec
+
+
 def spawn_ranks(n):
     """``--gpus n`` without a launcher: run this script under torch.distributed.run with n
     local ranks (RCCL rendezvous on 127.0.0.1) as a CHILD process — this process never
@@ -451,14 +463,19 @@ def main():
     # runs the N>1 code path (RCCL collectives on device tensors) end to end
     if world > 1 or os.environ.get("DSR_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
+        from reconstruct.parallel import rank_device
 
+        # rank r binds device r; under RCCL a node with fewer visible devices than ranks exits
+        # non-zero here instead of running its ranks on device 0 (parallel.rank_device)
+        local = rank_device(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), backend,
+                            torch.cuda.device_count())
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-            local = local % max(1, torch.cuda.device_count())
     coll_dev = torch.device("cuda", local) if backend == "nccl" and dist is not None else None
+    os.environ["DSR_DEVICE"] = str(local)        # Context.get() default: this rank's device
 
     from deep_sdf.workspace import decoder_from_state
     from reconstruct import _libdsr as L
@@ -517,14 +534,19 @@ def main():
     per_rank = [elapsed]
     ranks = {"world_size": world, "shard_objects": [len(s) for s in shard.shards],
              "gather_ms_per_step": round(gather_s / args.steps * 1e3, 4)}
+    me = device_record(dec.ctx.device, torch)
+    ranks["devices"] = [me]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev or "cpu")
         all_t = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(all_t, t)
         per_rank = [float(x.item()) for x in all_t]
         elapsed = max(per_rank)
+        devs = [None] * world
+        dist.all_gather_object(devs, me)
         ranks.update(backend=dist.get_backend(), world_size_observed=dist.get_world_size(),
-                     rank_seconds=[round(x, 4) for x in per_rank])
+                     rank_seconds=[round(x, 4) for x in per_rank], devices=devs,
+                     distinct_devices=len({(d["host"], d["pci_bus_id"], d["pci_domain_id"]) for d in devs}))
     if args.dump_records and rank == 0 and res is not None:
         np.save(args.dump_records, record_rows(res))
     value = n_job * args.steps / elapsed

@@ -69,11 +69,25 @@ static float* ln_workspace(dsr_ctx* ctx, int g) {
 // Forward-kernel variant (DSR_FWD_VARIANT: bit0 XCD soft sync, bit1 B prefetch, bit2 setprio,
 // bit3 split-fp16; 12 = split-fp16 + setprio, the default) and the A-ring depth of the split
 // kernels (DSR_SPLIT_RING: 0 = the two-set gemm16_tile, 2..4 = gemm16_ring k steps in flight)
+// Kernel-selecting switches (A/B experiments: DSR_FWD_VARIANT, DSR_JAC_VARIANT, DSR_SPLIT_RING,
+// DSR_LITE_VARIANT, DSR_LITE_LAG, DSR_REFINE_ALL, DSR_RENDER_PASSES, DSR_KEEP_MASKS,
+// DSR_SURFACE_EXACT) and the test hooks are read from the environment only under
+// DSR_TEST_HOOKS=1, which dsr_stats.test_hooks reports: a stray variable cannot change the kernels
+// of a production run (test_gpu_lite_audit.py: test_kernel_switches_ignored_without_the_gate).
+// The two production switches, DSR_STREAMS (object groups) and DSR_GRAPH (graph replay), are
+// reported in dsr_stats (n_groups, graph_mode); DSR_LITE=0 (every sample decoded exactly) in
+// dsr_stats.lite.
+static bool test_hooks() {
+  const char* e = getenv("DSR_TEST_HOOKS");
+  return e && atoi(e) != 0;
+}
+static const char* hook_env(const char* k) { return test_hooks() ? getenv(k) : nullptr; }
+
 #ifndef DSR_DEFAULT_SPLIT_RING
 #define DSR_DEFAULT_SPLIT_RING 2
 #endif
 static int split_ring() {
-  const char* e = getenv("DSR_SPLIT_RING");
+  const char* e = hook_env("DSR_SPLIT_RING");
   const int r = e ? atoi(e) : DSR_DEFAULT_SPLIT_RING;
   return (r >= 2 && r <= 4) ? r : 0;
 }
@@ -143,14 +157,18 @@ using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*,
 #ifndef DSR_DEFAULT_LITE_VARIANT
 #define DSR_DEFAULT_LITE_VARIANT 1496
 #endif
+static int lite_variant() {
+  const char* e = hook_env("DSR_LITE_VARIANT");
+  return e ? atoi(e) : DSR_DEFAULT_LITE_VARIANT;
+}
 static LiteKernel lite_kernel() {
-  const char* e = getenv("DSR_LITE_VARIANT");
-  switch (e ? atoi(e) : DSR_DEFAULT_LITE_VARIANT) {
+  switch (lite_variant()) {
 #ifdef DSR_LITE_EXPERIMENTS
+    // the barrier kernels and the scaled-epilogue staggered kernel read the split weights' hi
+    // pieces, which the shipped packing sign-alternates (SPLIT_ROW_SIGNS, off in this build)
     case 18: return k_mlp_fwd_lite<true, 18>;
     case 984: return k_mlp_fwd_lite_st<true, 88 + 256 + 512>;
     case 216: return k_mlp_fwd_lite_st<true, 88>;
-#endif
     case 16: return k_mlp_fwd_lite<true, 16>;
     case 32: return k_mlp_fwd_lite<true, 32>;
     case 40: return k_mlp_fwd_lite<true, 40>;
@@ -158,6 +176,7 @@ static LiteKernel lite_kernel() {
     case 56: return k_mlp_fwd_lite<true, 56>;
     case 24: return k_mlp_fwd_lite<true, 24>;
     case 88: return k_mlp_fwd_lite<true, 88>;
+#endif
     case 472: return k_mlp_fwd_lite_st<true, 88 + 256>;
   }
   return k_mlp_fwd_lite_st<true, 88 + 256 + 1024>;
@@ -165,30 +184,30 @@ static LiteKernel lite_kernel() {
 // DSR_REFINE_ALL=1: the exact pass re-decodes every band sample, also those behind a ray's
 // first certainly-full sample (k_refine_scan)
 static bool refine_all() {
-  const char* e = getenv("DSR_REFINE_ALL");
+  const char* e = hook_env("DSR_REFINE_ALL");
   return e && atoi(e) != 0;
 }
 // Test hooks (DSR_LITE_PERTURB, DSR_LITE_BREAK) change results or cost on purpose; the library
 // honours them only when DSR_TEST_HOOKS=1 was set as the batch was created, and reports that
 // in dsr_stats.test_hooks, so a stray variable cannot silently change a production run.
-static bool test_hooks() {
-  const char* e = getenv("DSR_TEST_HOOKS");
-  return e && atoi(e) != 0;
-}
 // DSR_LITE_LAG (staggered lite kernel): the k step group A reaches before group B starts a GEMM.
 // DSR_LITE_BREAK=1 (test hook): every block starts in the "broken" state of a timed-out
 // event wait, so every sample goes to the exact pass (lag -1)
 static int lite_lag(bool hooks) {
   const char* b = getenv("DSR_LITE_BREAK");
   if (hooks && b && atoi(b) != 0) return -1;
-  const char* e = getenv("DSR_LITE_LAG");
+  const char* e = hooks ? getenv("DSR_LITE_LAG") : nullptr;
   const int v = e ? atoi(e) : 4;
   return v < 0 ? 0 : (v > 7 ? 7 : v);
 }
 static int fwd_variant() {
-  const char* e = getenv("DSR_FWD_VARIANT");
+  const char* e = hook_env("DSR_FWD_VARIANT");
   return e ? atoi(e) : DSR_DEFAULT_FWD_VARIANT;
 }
+// the forward variant of a one-launch decoder query (dsr_sdf_eval, the mesher): the XCD soft-sync
+// variants (bit 0) need the per-batch sync counter these launches have not got, so their bit 0 is
+// dropped there (the same kernels otherwise)
+static int query_fwd_variant() { return fwd_variant() & ~1; }
 static int jac_variant();
 // the decoder variants (use_tanh, xyz_in_all) are implemented in the split-fp16 kernels only
 // (the fp32-MFMA A/B variants k_mlp_fwd / k_mlp_jac implement the shipped topology)
@@ -398,7 +417,9 @@ static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
     for (int t = 0; t < T; ++t)
       for (int lane = 0; lane < 64; ++lane)
         for (int j = 0; j < 8; ++j) {
-          const float x = std::ldexp(src(16 * rb + (lane & 15), 32 * t + 8 * (lane >> 4) + j), sw);
+          // odd 16-row blocks negated (SPLIT_ROW_SIGNS, dsr_mlp16.hpp: row_sign)
+          const float sg = (SPLIT_ROW_SIGNS && (rb & 1)) ? -1.f : 1.f;
+          const float x = sg * std::ldexp(src(16 * rb + (lane & 15), 32 * t + 8 * (lane >> 4) + j), sw);
           const _Float16 h = (_Float16)x;
           const _Float16 l = (_Float16)(x - (float)h);
           out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = h;
@@ -673,7 +694,7 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // A batch whose first 16-rank window would spill just past one round of lite tiles (n_cu
 // 128-point tiles: one KITTI-sized object per call) gets a first window that fits that round.
 static std::vector<int> render_passes(int M, long samples, long rays, int n_cu) {
-  const char* e = getenv("DSR_RENDER_PASSES");
+  const char* e = hook_env("DSR_RENDER_PASSES");
   std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : samples >= 100000 ? "16,24" : "0");
   const long round = (long)n_cu * LTILE;
   if (!e && spec == "16,24" && rays > 0 && rays * 16 > round && rays * 12 <= round)
@@ -918,7 +939,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     b->lite = !(e && atoi(e) == 0) && !(fwd_variant() & 1) && dec->info.lite_eligible;
   }
   if (b->lite) {
-    const char* km = getenv("DSR_KEEP_MASKS");
+    const char* km = hook_env("DSR_KEEP_MASKS");
     if (!(km && atoi(km) == 0)) {     // 512 B of masks per sample of the worst case: HBM is ample
       // slots: the samples' (cand order), then the surface points' (MaskArgs.surf_base)
       ALLOC(b->ma.msk, sizeof(uint16_t) * 256 * ((size_t)cand_off + pts_off));
@@ -930,7 +951,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
       // kernel chains only backward passes: bitwise the same results; it shortens small
       // batches' chains (8-object Redwood keyframe -7%) and costs 64-object batches ~1%
       // (the forward moves, the MFMA work is equal).  DSR_SURFACE_EXACT=0/1 overrides.
-      const char* se = getenv("DSR_SURFACE_EXACT");
+      const char* se = hook_env("DSR_SURFACE_EXACT");
       const bool surf = se ? atoi(se) != 0 : n_obj <= 16;
       if (surf && fwd_variant() == 12) {
         b->ma.pts = b->pts;
@@ -1146,7 +1167,7 @@ static int batch_enqueue(dsr_batch* b, bool timing = true);
 static int batch_finish(dsr_batch* b);
 
 static int jac_variant() {
-  const char* e = getenv("DSR_JAC_VARIANT");
+  const char* e = hook_env("DSR_JAC_VARIANT");
   return e ? atoi(e) : 12;
 }
 
@@ -1474,6 +1495,12 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->lite_safety = b->P.lite_safety;
   st->graph_captures = b->captures;
   st->graph_replays = b->replays;
+  st->n_groups = (int)b->groups.size();
+  st->graph_mode = b->cap_graph ? 2 : (graph_enabled() ? 1 : 0);
+  st->fwd_variant = fwd_variant();
+  st->jac_variant = jac_variant();
+  st->lite_variant = b->lite ? lite_variant() : 0;
+  st->split_ring = split_ring();
   {
     int nb = 0;
     DSR_CHECK(b->ctx, hipMemcpy(&nb, b->diag + STD_BROKEN, sizeof(int), hipMemcpyDeviceToHost));
@@ -1742,7 +1769,10 @@ static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec) {
   E.diag = nullptr;
   hipLaunchKernelGGL(lite_kernel(), dim3(ctx->n_cu), dim3(512), 0, st, D, (const Tile*)dtl, (const int*)dntl,
                      (const ObjDesc*)ddesc, (const float4*)dc, (const float*)db0, (const float*)db4, dl, E);
-  hipLaunchKernelGGL(fwd_kernel(fwd_variant()), dim3(ctx->n_cu), dim3(512), 0, st, D, (const Tile*)dte,
+  // against the split-fp16 exact pass a lite batch runs (fwd_kernel(12)), whatever a test's
+  // DSR_FWD_VARIANT selects: the XCD soft-sync variants (bit 0) need a sync counter this launch
+  // has not got, and batches on them never run the lite pass anyway
+  hipLaunchKernelGGL(fwd_kernel(12), dim3(ctx->n_cu), dim3(512), 0, st, D, (const Tile*)dte,
                      (const int*)dnte, (const ObjDesc*)ddesc, (const float4*)dc, (const float*)db0,
                      (const float*)db4, de, (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr},
                      MaskArgs{nullptr, nullptr, nullptr, nullptr});
@@ -1896,7 +1926,7 @@ int dsr_mesher_run(dsr_mesher* m, const float* code, float level, float* verts, 
   DSR_CHECK(ctx, hipMemcpyAsync(m->code, zc, sizeof(float) * CODE, hipMemcpyHostToDevice, s));
   DSR_CHECK(ctx, hipStreamSynchronize(s));          // (zc is on this stack frame)
   hipLaunchKernelGGL(k_fold_code, dim3(HID / 256), dim3(256), 0, s, D, (const float*)m->code, m->b0, m->b4);
-  hipLaunchKernelGGL(fwd_kernel_for(D, fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
+  hipLaunchKernelGGL(fwd_kernel_for(D, query_fwd_variant()), dim3(std::min(ctx->n_cu, m->nt)), dim3(512), 0, s, D,
                      (const Tile*)m->tiles, (const int*)m->ntiles, (const ObjDesc*)m->desc, (const float4*)m->pts,
                      (const float*)m->b0, (const float*)m->b4, m->vol, (unsigned*)nullptr,
                      ErtArgs{nullptr, 1, 0.f, nullptr, nullptr}, MaskArgs{nullptr, nullptr, nullptr, nullptr});
@@ -2010,7 +2040,7 @@ int dsr_sdf_eval(dsr_ctx* ctx, const dsr_decoder* dec, const float* code, const 
                        (float*)nullptr, (const float4*)dp, (float*)dout, (float*)nullptr,
                        MaskArgs{nullptr, nullptr, nullptr, nullptr}, lnw);
   } else {
-    hipLaunchKernelGGL(fwd_kernel_for(D, fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
+    hipLaunchKernelGGL(fwd_kernel_for(D, query_fwd_variant()), dim3(grid), dim3(512), 0, s, D, (const Tile*)dt, (const int*)dnt,
                        (const ObjDesc*)dd, (const float4*)dp, (const float*)db0, (const float*)db4, (float*)dout,
                        (unsigned*)nullptr, ErtArgs{nullptr, 1, 0.f, nullptr, nullptr},
                        MaskArgs{nullptr, nullptr, nullptr, nullptr});

@@ -81,7 +81,10 @@ struct DevDecoder {
 // normalised activations x^ (acc layout, [16 (q, cb)][512 threads] float4) and rstd per point,
 // written by the forward and read back by the backward of the same tile
 constexpr int LN_WS_LAYER = 16 * 512 * 4 + 64;     // floats
-constexpr int LN_WS_WG = 8 * LN_WS_LAYER;          // floats per workgroup (1.0 MB)
+constexpr int LN_WS_WG = 8 * LN_WS_LAYER;          // floats per workgroup (4.2 MB: 8 layers x 16 float4
+                                                   // x 512 threads + rstd); n_cu of them per stream, so
+                                                   // ~1.3 GB per object-group stream on 304 CUs, allocated
+                                                   // only for LayerNorm decoders (never DSP-SLAM's)
 
 // row of the point's xyz in the input of the layer after lin_l (l = 0..7), or -1: lin4's input
 // is [h3 | code (folded) | xyz] (row l3), with xyz_in_all every other layer's is [h | xyz] (509)

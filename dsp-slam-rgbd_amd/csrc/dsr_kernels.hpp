@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[q][cb][r] = __builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r));
+              for (int r = 0; r < 4; ++r) v[q][cb][r] = __builtin_fmaf(accr(acc[q][cb], r), usc * rc_sign(q, cb), fetch4(bb, r));
           }
           ln_fwd(v, D.ln_g[l], D.ln_b[l], D.ln_dim[l], sm.red, sm.red2, w, lane, lnw + (size_t)l * LN_WS_LAYER);
 #pragma unroll
@@ -1399,7 +1399,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           for (int cb = 0; cb < 4; ++cb) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc, fetch4(bb, r)), 0.f);
+              const float h = fmaxf(__builtin_fmaf(accr(acc[q][cb], r), usc * rc_sign(q, cb), fetch4(bb, r)), 0.f);
               if (h > 0.f) bits |= 1ull << ((q * 4 + cb) * 4 + r);
               v[q][cb][r] = h;
               m = fmaxf(m, h);
@@ -1431,7 +1431,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un);
+            for (int r = 0; r < 4; ++r) acc[q][cb][r] = ldexpf(acc[q][cb][r], -un) * rc_sign(q, cb);
         const bool ln7 = VAR && ((D.ln_mask >> 7) & 1);
         if (ln7) ln_l7(acc, D, sm.red, sm.red2, w, lane, lnw + (size_t)7 * LN_WS_LAYER);
         epi_l7(acc, D, sm.red, w, lane, mk[7], VAR ? sm.xyz : nullptr, !ln7);
@@ -1502,7 +1502,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       [&]<int... K>(std::integer_sequence<int, K...>) {
         ([&] {
           constexpr int q = K >> 4, cb = (K >> 2) & 3, r = K & 3;
-          const float gv = keep_if<K>(accr(acc[q][cb], r) * usc, mask);   // exact (power of two)
+          const float gv = keep_if<K>(accr(acc[q][cb], r) * (usc * rc_sign(q, cb)), mask);   // exact (power of two)
           v[q][cb][r] = gv;
           m = fmaxf(m, fabsf(gv));
         }(), ...);
@@ -1514,7 +1514,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
         for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
           for (int r = 1; r < 4; ++r) {
-            xg[cb][r - 1] += accr(acc[3][cb], r) * usc;
+            xg[cb][r - 1] += accr(acc[3][cb], r) * (usc * rc_sign(3, cb));
             v[3][cb][r] = 0.f;
           }
       }
@@ -1537,7 +1537,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
             for (int r = 0; r < 4; ++r) {
               const int n = 64 * w + 16 * q + 4 * g + r;
               if (n >= D.l3) {
-                sm.gin[p * GIN_PITCH + gin_slot(n, D.l3)] = accr(acc[q][cb], r) * usc;
+                sm.gin[p * GIN_PITCH + gin_slot(n, D.l3)] = accr(acc[q][cb], r) * (usc * rc_sign(q, cb));
                 v[q][cb][r] = 0.f;
               }
             }
@@ -1568,7 +1568,8 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
           const int n = 16 * w + 4 * g + r;
           if (n < IN)
             sm.gin[p * GIN_PITCH + n] =
-                ldexpf(accr(a1[0][cb], r), -un) + ((n >= D.code_len && n < CODE) ? 0.f : sm.gin[p * GIN_PITCH + n]);
+                ldexpf(accr(a1[0][cb], r), -un) * rc_sign(w, cb) +
+                ((n >= D.code_len && n < CODE) ? 0.f : sm.gin[p * GIN_PITCH + n]);
         }
       }
     }
@@ -1681,7 +1682,11 @@ __device__ inline float rotation_prior(const float* Tco, float* jrot) {
     return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
            m[2] * (m[3] * m[7] - m[4] * m[6]);
   };
-  const double sc = cbrt(det(r3));
+  // torch.det(r_co) ** (1/3) (loss.py:177): NaN for a negative determinant (a reflected pose), and
+  // the NaN flows into b as it does there (the next iteration then fails like the reference's);
+  // cbrt alone would return a finite negative scale
+  const double d0 = det(r3);
+  const double sc = d0 < 0.0 ? (double)__builtin_nan("") : cbrt(d0);
   for (int i = 0; i < 9; ++i) r3[i] /= sc;
   const double dr = det(r3);
   const double res_rot = 1.0 - (-r3[1 * 3 + 1]);             // 1 - (R_co e_y).n_g

@@ -68,7 +68,7 @@ class Trace(C.Structure):
                 ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
 
 
-ABI_VERSION = 9          # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 10         # include/dsr.h DSR_ABI_VERSION
 BATCH_GRAPH = 1          # include/dsr.h DSR_BATCH_GRAPH
 
 
@@ -85,7 +85,9 @@ class Stats(C.Structure):
                 ("lite_broken_blocks", C.c_int), ("test_hooks", C.c_int),
                 ("lite_eligible", C.c_int), ("audit", C.c_int), ("audit_shell", C.c_float),
                 ("audit_log2", C.c_int), ("lite_margin0", C.c_float), ("lite_floor", C.c_float),
-                ("lite_safety", C.c_float), ("graph_captures", C.c_int), ("graph_replays", C.c_int)]
+                ("lite_safety", C.c_float), ("graph_captures", C.c_int), ("graph_replays", C.c_int),
+                ("n_groups", C.c_int), ("graph_mode", C.c_int), ("fwd_variant", C.c_int),
+                ("jac_variant", C.c_int), ("lite_variant", C.c_int), ("split_ring", C.c_int)]
 
 
 class DecoderInfo(C.Structure):

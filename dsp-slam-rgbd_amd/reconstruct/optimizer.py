@@ -189,28 +189,51 @@ class Optimizer(object):
         return self.reconstruct_keyframe_async(detections).wait()
 
     MAX_SLOTS = 4
+    # A slot batch is laid out for max_obj x max_rays x M ray samples whatever the fill, and every
+    # run launches its render chunks over that capacity (~580 B of device memory per sample with
+    # the kept ReLU masks).  A keyframe only uses a slot whose capacity is at most SLOT_WASTE x its
+    # own ray count (or SLOT_MIN_RAYS), a slot only grows while it stays inside that bound, and no
+    # slot exceeds SLOT_MAX_SAMPLES ray samples (2^24: ~9.7 GB); otherwise the keyframe runs as a
+    # one-shot batch (INTEGRATION.md §2 states the bound)
+    SLOT_WASTE = 4.0
+    SLOT_MIN_RAYS = 8 * 1024
+    SLOT_MAX_SAMPLES = 1 << 24
+
+    def _slot_ok(self, n_obj, n_rays_cap, real_rays):
+        cap = n_obj * n_rays_cap
+        return (cap <= max(self.SLOT_WASTE * real_rays, self.SLOT_MIN_RAYS)
+                and cap * self.num_depth_samples <= self.SLOT_MAX_SAMPLES)
 
     def _slot_for(self, objects):
         """A free fixed-capacity batch (dsr_batch_create_capacity) that holds ``objects``, or
-        None (``keyframe_mode`` "oneshot", or every slot busy with an in-flight keyframe)."""
+        None (``keyframe_mode`` "oneshot", every slot busy with an in-flight keyframe, or no slot
+        within the capacity bounds above: the keyframe then runs as a one-shot batch)."""
         if self.keyframe_mode not in ("slot", "graph") or not objects:
             return None
         n = len(objects)
+        rays = [_f32(ob[2], 3).shape[0] for ob in objects]
         need_p = max(_f32(ob[1], 3).shape[0] for ob in objects)
-        need_r = max(_f32(ob[2], 3).shape[0] for ob in objects)
+        need_r = max(rays)
+        real = sum(rays)
         graph = self.keyframe_mode == "graph"
         free = [sl for sl in self._slots if not sl.busy and sl.graph == graph]
         for sl in free:
-            if sl.fits(n, need_p, need_r):
+            if sl.fits(n, need_p, need_r) and self._slot_ok(sl.max_obj, sl.max_rays, real):
                 return sl
-        if free:                                     # grow the first free slot
+        pad = lambda v: -(-v // 128) * 128  # noqa: E731
+        cn, cp, cr = n, pad(need_p), pad(need_r)
+        if free:                                     # grow the first free slot, or replace it
             old = free[0]
+            gn, gp, gr = max(cn, old.max_obj), max(cp, old.max_pts), max(cr, old.max_rays)
+            if self._slot_ok(gn, gr, real):
+                cn, cp, cr = gn, gp, gr
             self._slots.remove(old)
             old.close()
-            n, need_p, need_r = max(n, old.max_obj), max(need_p, old.max_pts), max(need_r, old.max_rays)
         elif len(self._slots) >= self.MAX_SLOTS:
             return None
-        sl = SlotBatch(self, n, -(-need_p // 128) * 128, -(-need_r // 128) * 128, graph)
+        if not self._slot_ok(cn, cr, real):
+            return None
+        sl = SlotBatch(self, cn, cp, cr, graph)
         self._slots.append(sl)
         return sl
 

@@ -20,6 +20,22 @@ import numpy as np
 REC = 96
 
 
+def rank_device(local_rank, local_world, backend, device_count):
+    """The HIP device a local rank binds: rank r -> device r.  RCCL ("nccl") needs one GPU per
+    rank, so a node whose ranks outnumber its visible devices is an error (a mis-bound launch
+    would otherwise put several ranks on device 0 and measure nothing); gloo (the CPU
+    rehearsals) shares the visible devices round-robin."""
+    local_rank, local_world, device_count = int(local_rank), int(local_world), int(device_count)
+    if not 0 <= local_rank < max(1, local_world):
+        raise RuntimeError(f"local rank {local_rank} outside the node's {local_world} ranks")
+    if backend == "nccl":
+        if device_count < local_world:
+            raise RuntimeError(f"{local_world} ranks on this node but only {device_count} visible HIP "
+                               "device(s): RCCL needs one GPU per rank (check HIP_VISIBLE_DEVICES)")
+        return local_rank
+    return local_rank % max(1, device_count)
+
+
 def lpt_partition(costs, world):
     """Indices per rank, longest-processing-time-first (deterministic)."""
     order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 9
+#define DSR_ABI_VERSION 10
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -169,6 +169,16 @@ typedef struct {
   float lite_safety;
   int graph_captures;             /* hipGraph captures / replays over the batch's life */
   int graph_replays;
+  /* ---- the kernels and launch structure this batch ran (ABI 10) ---- */
+  int n_groups;                   /* object groups on concurrent streams (DSR_STREAMS or the default) */
+  int graph_mode;                 /* 0 eager, 1 DSR_GRAPH=1 (re-runs replay a graph), 2 a
+                                     DSR_BATCH_GRAPH capacity batch */
+  int fwd_variant;                /* exact-pass kernel (12: split-fp16, the shipped kernel) */
+  int jac_variant;                /* Jacobian kernel (12: split-fp16) */
+  int lite_variant;               /* lite-pass kernel (1496 shipped; 0 when the lite pass is off) */
+  int split_ring;                 /* A-ring depth of the split kernels (2 shipped).  Only under
+                                     DSR_TEST_HOOKS=1 can DSR_FWD_VARIANT / _JAC_VARIANT /
+                                     _LITE_VARIANT / _SPLIT_RING move these from the shipped values */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */

@@ -258,6 +258,7 @@ def test_batch_equals_single(gpu_decoder, streams, monkeypatch):
     pinned here so that each object-group count runs the same windows; that the default
     schedules themselves change no bit is test_default_schedules_give_bitwise_equal_results."""
     monkeypatch.setenv("DSR_STREAMS", streams)
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
     monkeypatch.setenv("DSR_RENDER_PASSES", "16,24")
     opt = _opt(gpu_decoder, dict(S.REDWOOD_OPTIM, joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"],
                                                                     num_iterations=3)), "Redwood")
@@ -296,6 +297,7 @@ def test_default_schedules_give_bitwise_equal_results(gpu_decoder, monkeypatch):
     runs = {"batch16": opt.reconstruct_objects(objs, trace=True),
             "batch8": opt.reconstruct_objects(objs[:8], trace=True)}
     singles = [opt.reconstruct_objects([ob], trace=True) for ob in objs[:3]]
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
     monkeypatch.setenv("DSR_RENDER_PASSES", "0")
     runs["one_pass"] = opt.reconstruct_objects(objs[:8], trace=True)
     ref_res, ref_tr = runs["batch8"]
@@ -508,6 +510,7 @@ def test_early_ray_termination_matches_full_decode(gpu_decoder, monkeypatch):
     out = {}
     # (the large-batch default, the small-batch default, a fine schedule)
     for spec in ("0", "8,12,16,20,24,32", "16,24", "4,5,6,7,8,9,10,11,12,14,16,20,24,28,32,40"):
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_RENDER_PASSES", spec)
         out[spec] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
     full_res, full_tr = out["0"]
@@ -525,6 +528,7 @@ def test_early_ray_termination_matches_full_decode(gpu_decoder, monkeypatch):
     pts = {}
     monkeypatch.setenv("DSR_STREAMS", "1")
     for spec in ("0", "8,12,16,20,24,32"):
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_RENDER_PASSES", spec)
         h, keep = bench.make_batch(gpu_decoder, params, 8, 1000)
         lib, ctx = gpu_decoder.ctx.lib, gpu_decoder.ctx
@@ -706,6 +710,7 @@ def test_lite_pass_matches_exact_decode(gpu_decoder, monkeypatch):
     # exact decode | lite + exact band, Jacobian re-forwards render points | ... masks kept
     for lite, keep in (("0", "1"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("DSR_LITE", lite)
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_KEEP_MASKS", keep)
         out[lite + keep] = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
     r0, t0 = out["01"]
@@ -749,6 +754,7 @@ def test_refine_stops_at_ray_termination(gpu_decoder, monkeypatch):
     monkeypatch.setenv("DSR_LITE", "1")
     sig = {}
     for mode in ("1", "0"):
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_REFINE_ALL", mode)
         h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
         try:
@@ -785,6 +791,7 @@ def test_lite_staggered_groups_bitwise(gpu_decoder, monkeypatch):
     monkeypatch.setenv("DSR_LITE", "1")
     sig = {}
     for v, lag in (("1496", "4"), ("1496", "0"), ("1496", "7"), ("472", "4")):
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_LITE_VARIANT", v)
         monkeypatch.setenv("DSR_LITE_LAG", lag)
         h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 8, 1000)
@@ -877,6 +884,7 @@ def test_surface_forward_in_exact_pass_bitwise(gpu_decoder, monkeypatch):
     monkeypatch.setenv("DSR_LITE", "1")
     sig = {}
     for mode in ("0", "1"):
+        monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
         monkeypatch.setenv("DSR_SURFACE_EXACT", mode)
         h, keep = bench.make_batch(gpu_decoder, L.optim_params(S.KITTI_OPTIM), 6, 1000)
         try:

@@ -138,7 +138,9 @@ def test_variant_refused_on_the_fp32_kernels(decs, monkeypatch):
     from reconstruct.optimizer import sdf_eval
 
     f = golden("f17_variants.npz")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
     monkeypatch.setenv("DSR_FWD_VARIANT", "0")
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
     monkeypatch.setenv("DSR_JAC_VARIANT", "0")
     for v in ("tanh", "xyz", "ln"):
         with pytest.raises(L.DsrError):

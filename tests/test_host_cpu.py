@@ -293,3 +293,58 @@ def test_unsupported_decoder_variants_rejected_loudly(change, what):
     with pytest.raises(NotImplementedError, match="shapes"):
         check_topology(specs, layers)
     check_topology(specs, fold_state(S.make_decoder(1234, specs), specs))
+
+
+def test_keyframe_slot_capacity_is_bounded(monkeypatch):
+    """a keyframe slot batch is laid out for max_obj x max_rays x M ray samples
+    whatever the fill.  A slot serves a keyframe only within SLOT_WASTE x the keyframe's own ray
+    count, grows only inside that bound, and never beyond SLOT_MAX_SAMPLES — otherwise the
+    keyframe runs one-shot (``_slot_for`` returns None).  SlotBatch is stubbed: no device here."""
+    from reconstruct import optimizer as O
+    from conftest import make_cfg
+
+    made = []
+
+    class Stub:
+        def __init__(self, opt, max_obj, max_pts, max_rays, graph):
+            self.max_obj, self.max_pts, self.max_rays, self.graph = max_obj, max_pts, max_rays, graph
+            self.busy = False
+            self.closed = False
+            made.append(self)
+
+        def fits(self, n, p, r):
+            return n <= self.max_obj and p <= self.max_pts and r <= self.max_rays
+
+        def close(self):
+            self.closed = True
+
+    monkeypatch.setattr(O, "SlotBatch", Stub)
+    monkeypatch.setattr(O.Optimizer, "SLOT_MIN_RAYS", 256)
+    opt = O.Optimizer(None, make_cfg(S.REDWOOD_OPTIM, "Redwood"))
+    assert opt.keyframe_mode == "graph"
+
+    def kf(n, n_pts, n_rays):
+        return [(np.eye(4), np.zeros((n_pts, 3)), np.zeros((n_rays, 3)), np.zeros(0)) for _ in range(n)]
+
+    many_small = opt._slot_for(kf(8, 256, 300))        # 8 x 384 rays padded
+    assert (many_small.max_obj, many_small.max_rays) == (8, 384)
+    # one large object: growing the 8-object slot to 8 x 4096 rays would be 8x its need -> a new
+    # slot sized for it replaces the free one
+    big = opt._slot_for(kf(1, 2048, 4000))
+    assert (big.max_obj, big.max_rays) == (1, 4096) and many_small.closed
+    # a small keyframe inside the large slot's bound is served by it
+    assert opt._slot_for(kf(1, 100, 1500)) is big
+    # a keyframe far smaller than every free slot does not use them: a slot of its own
+    tiny = opt._slot_for(kf(1, 64, 100))
+    assert tiny is not big and (tiny.max_obj, tiny.max_rays) == (1, 128)
+    # beyond SLOT_MAX_SAMPLES ray samples: one-shot
+    monkeypatch.setattr(O.Optimizer, "SLOT_MAX_SAMPLES", 1 << 16)
+    for sl in opt._slots:
+        sl.busy = True
+    assert opt._slot_for(kf(4, 1024, 2048)) is None
+    # every slot busy and MAX_SLOTS reached: one-shot
+    monkeypatch.setattr(O.Optimizer, "SLOT_MAX_SAMPLES", 1 << 24)
+    while len(opt._slots) < opt.MAX_SLOTS:
+        opt._slots.append(Stub(opt, 1, 128, 128, True))
+        opt._slots[-1].busy = True
+    assert opt._slot_for(kf(1, 64, 100)) is None

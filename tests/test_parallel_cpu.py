@@ -303,3 +303,50 @@ def test_sharded_equals_single_process():
         assert it == r["iters_done"]
         if good:
             assert np.array_equal(np.asarray(T, np.float32), np.asarray(r["t_cam_obj"], np.float32))
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_rank_r_binds_device_r(world, monkeypatch):
+    """at N = 8 rank r runs on HIP device r — bench.py binds it through
+    parallel.rank_device (and exports it as DSR_DEVICE), the library's Context.get() default
+    reads DSR_DEVICE / LOCAL_RANK — and an RCCL launch on a node with fewer visible devices than
+    ranks exits with a message instead of running its ranks on device 0 (device count mocked)."""
+    from reconstruct import _libdsr as L
+    from reconstruct.parallel import rank_device
+
+    for r in range(world):
+        assert rank_device(r, world, "nccl", 8) == r
+        assert rank_device(r, world, "gloo", 1) == 0          # CPU rehearsals share device 0
+    if world > 1:
+        with pytest.raises(RuntimeError, match="one GPU per rank"):
+            rank_device(world - 1, world, "nccl", world - 1)
+    with pytest.raises(RuntimeError):
+        rank_device(world, world, "nccl", 8)
+
+    made = []
+
+    def fake_init(self, device=0):
+        self.device = device
+        self.handle = None
+        made.append(device)
+
+    monkeypatch.setattr(L.Context, "__init__", fake_init)
+    monkeypatch.setattr(L.Context, "_cache", {})
+    monkeypatch.delenv("DSR_DEVICE", raising=False)
+    for r in range(world):
+        monkeypatch.setenv("LOCAL_RANK", str(r))
+        assert L.Context.get().device == r
+        monkeypatch.setenv("DSR_DEVICE", str(r))               # what bench.py exports after binding
+        assert L.Context.get().device == r
+        monkeypatch.delenv("DSR_DEVICE")
+    assert made == list(range(world))
+
+
+def test_bench_binds_through_rank_device():
+    """bench.py routes its rank -> device binding through parallel.rank_device (the checked
+    helper above) before any process group or context exists, and records every rank's device."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    i_bind = src.index("local = rank_device(")
+    assert i_bind < src.index("torch.cuda.set_device(local)") < src.index('dist.init_process_group("nccl"')
+    assert 'os.environ["DSR_DEVICE"] = str(local)' in src
+    assert "all_gather_object(devs, me)" in src and "distinct_devices" in src
