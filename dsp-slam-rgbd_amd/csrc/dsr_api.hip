@@ -401,10 +401,38 @@ static void pack_frag(std::vector<float>& out, int rows_pad, int cols_pad,
               src(16 * rb + (lane & 15), 16 * t + 4 * (lane >> 4) + j);
 }
 
+// The fp16 neighbour of h on the other side of r (h = fp16(r) != r): one step up or down the fp16
+// grid, by the bit pattern (sign-magnitude; +0 / -0 step to the smallest subnormals)
+static _Float16 f16_other_side(_Float16 h, double r) {
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  const bool up = (double)h < r;                    // r lies above h: the next value up
+  const bool neg = (b & 0x8000) != 0, zero = (b & 0x7fff) == 0;
+  if (zero) b = up ? 0x0001 : 0x8001;
+  else if (up != neg) b = (uint16_t)(b + 1);        // away from zero
+  else b = (uint16_t)(b - 1);                       // toward zero
+  _Float16 o;
+  std::memcpy(&o, &b, 2);
+  return o;
+}
+
 // Split-fp16 A fragments for v_mfma_f32_16x16x32_f16 (dsr_mlp16.hpp):
 // out[(((rb*T + t)*2 + piece)*64 + lane)*8 + j] = piece of src(16 rb + (lane&15), 32 t + 8 (lane>>4) + j) * 2^sw
+// hi = fp16(W 2^sw) and lo = one of the two fp16 neighbours of the remainder W 2^sw - hi.  With
+// `hbar` (the mean of each GEMM input column over a probe set, decoder_input_means) lo is chosen by
+// error feedback along each row — the neighbour that keeps sum_c (hi + lo - W 2^sw)_c hbar_c
+// closest to zero — instead of to nearest: hi + lo carries 22-23 of an fp32 weight's 24 bits, and
+// the rounded-away tails are a FIXED perturbation of the decoder, a smooth function of x that puts
+// the same offset on every nearby point's sdf (-2.3e-8 on the bench decoder, numpy emulation;
+// -2e-8 measured on the GPU, tools/bias_probe.py), which the sdf term's b = sum J r adds up.
+// Feedback rounding leaves each row's pre-activation offset at its mean input near zero (emulated:
+// -2.5e-9, a ninth).  Without hbar: round to nearest (the backward packs).
+// `tail` (non-null): also the third pieces fp16(W 2^sw - hi - lo) in the one-piece fragment layout
+// [rb][t][64 lanes] x 8 halfs (gemm16_tail): hi + lo + tail carries an fp32 weight exactly (tails
+// below the fp16 subnormals of weights ~2^-14 of the layer's largest excepted).
 static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
-                       const std::function<float(int, int)>& src) {
+                       const std::function<float(int, int)>& src, const std::vector<double>* hbar = nullptr,
+                       std::vector<_Float16>* tail = nullptr) {
   float mx = 0.f;
   for (int r = 0; r < rows_pad; ++r)
     for (int c = 0; c < cols_pad; ++c) mx = std::max(mx, std::fabs(src(r, c)));
@@ -413,22 +441,167 @@ static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
   const int sw = 14 - e;                            // max |W| * 2^sw < 2^14
   const int RB = rows_pad / 16, T = cols_pad / 32;
   out.assign((size_t)RB * T * 2 * 64 * 8, (_Float16)0.f);
-  for (int rb = 0; rb < RB; ++rb)
+  if (tail) tail->assign((size_t)RB * T * 64 * 8, (_Float16)0.f);
+  std::vector<_Float16> hi((size_t)cols_pad), lo((size_t)cols_pad), tl((size_t)cols_pad);
+  for (int r = 0; r < rows_pad; ++r) {
+    double acc = 0.0;                               // the row's running sum of (hi + lo - x) hbar
+    for (int c = 0; c < cols_pad; ++c) {
+      const float x = std::ldexp(src(r, c), sw);
+      const _Float16 h = (_Float16)x;
+      const double rem = (double)x - (double)(float)h;   // exact
+      _Float16 l = (_Float16)(float)rem;                 // to nearest (rem is exact in fp32)
+      if (hbar && (double)(float)l != rem) {
+        const _Float16 l2 = f16_other_side(l, rem);
+        const double w = (*hbar)[c];
+        const double e1 = acc + ((double)(float)l - rem) * w, e2 = acc + ((double)(float)l2 - rem) * w;
+        if (std::fabs(e2) < std::fabs(e1)) l = l2;
+      }
+      acc += ((double)(float)l - rem) * (hbar ? (*hbar)[c] : 0.0);
+      hi[c] = h;
+      lo[c] = l;
+      tl[c] = (_Float16)(float)(rem - (double)(float)l);   // exact difference, rounded once
+    }
+    const int rb = r >> 4, lr = r & 15;
+    // odd 16-row blocks negated (SPLIT_ROW_SIGNS, dsr_mlp16.hpp: row_sign): exact, both pieces
+    const bool neg = SPLIT_ROW_SIGNS && (rb & 1);
     for (int t = 0; t < T; ++t)
-      for (int lane = 0; lane < 64; ++lane)
+      for (int g = 0; g < 4; ++g)
         for (int j = 0; j < 8; ++j) {
-          // odd 16-row blocks negated (SPLIT_ROW_SIGNS, dsr_mlp16.hpp: row_sign)
-          const float sg = (SPLIT_ROW_SIGNS && (rb & 1)) ? -1.f : 1.f;
-          const float x = sg * std::ldexp(src(16 * rb + (lane & 15), 32 * t + 8 * (lane >> 4) + j), sw);
-          const _Float16 h = (_Float16)x;
-          const _Float16 l = (_Float16)(x - (float)h);
-          out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = h;
-          out[((((size_t)rb * T + t) * 2 + 1) * 64 + lane) * 8 + j] = l;
+          const int c = 32 * t + 8 * g + j, lane = lr + 16 * g;
+          out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = neg ? (_Float16)(-hi[c]) : hi[c];
+          out[((((size_t)rb * T + t) * 2 + 1) * 64 + lane) * 8 + j] = neg ? (_Float16)(-lo[c]) : lo[c];
+          if (tail) (*tail)[(((size_t)rb * T + t) * 64 + lane) * 8 + j] = neg ? (_Float16)(-tl[c]) : tl[c];
         }
+  }
   return sw;
 }
 
 static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec);
+
+// Mean input of each split forward GEMM (lin1..lin7) over a fixed probe set — 256 points uniform
+// in the unit ball (fixed LCG), code 0 — in the packed column order pack_frag16 uses: lin l's
+// columns are its input h_{l-1} (with xyz at 509..511 under xyz_in_all); lin4's are h3 (l3) then
+// xyz (the code is folded into its bias).  A host forward pass of deep_sdf_decoder.py:75-110 in
+// fp32 (LayerNorm and xyz_in_all included), split over host threads; ~0.1 s once per load.
+// With `gbar` (non-null, decoders without LayerNorm): also the mean of d sdf / d(pre-activation of
+// lin l) (masked by its ReLU) for l = 0..7 — the input of the backward GEMM W_l^T, in its packed
+// column order (lin l's outputs) — for the backward packs' feedback rounding.
+static std::vector<std::vector<double>> decoder_input_means(const int* od, const int* id, const std::vector<const float*>& W,
+                                                            const std::vector<const float*>& B,
+                                                            const std::vector<const float*>& LG,
+                                                            const std::vector<const float*>& LB, int L, int l3, int XA,
+                                                            int K4, int use_tanh = 0,
+                                                            std::vector<std::vector<double>>* gbar = nullptr) {
+  constexpr int P = 256;
+  std::vector<float> pts((size_t)P * 3);
+  uint64_t s = 0xD1B54A32D192ED03ull;
+  auto u01 = [&]() {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)(s >> 11) * (1.0 / 9007199254740992.0);
+  };
+  for (int i = 0; i < P;) {
+    const double x = 2 * u01() - 1, y = 2 * u01() - 1, z = 2 * u01() - 1;
+    if (x * x + y * y + z * z >= 1.0) continue;
+    pts[3 * i] = (float)x; pts[3 * i + 1] = (float)y; pts[3 * i + 2] = (float)z;
+    ++i;
+  }
+  constexpr int nth = 8;      // fixed (not the host's core count): the means, hence the packs, are the same on every host
+  std::vector<std::vector<std::vector<double>>> part(nth, std::vector<std::vector<double>>(8));
+  std::vector<std::vector<std::vector<double>>> gpart(nth, std::vector<std::vector<double>>(8));
+  auto work = [&](int th) {
+    auto& sums = part[th];
+    for (int l = 1; l <= 7; ++l) sums[l].assign(l == 4 ? K4 : 512, 0.0);
+    for (int l = 0; l <= 7; ++l) gpart[th][l].assign(512, 0.0);
+    std::vector<float> h, in, a;
+    std::vector<std::vector<float>> ins(9), pre(9);
+    for (int p = th; p < P; p += nth) {
+      const float* xyz = &pts[3 * p];
+      std::vector<float> inp((size_t)L + 3, 0.f);  // [code (0) | xyz]
+      inp[L] = xyz[0]; inp[L + 1] = xyz[1]; inp[L + 2] = xyz[2];
+      h = inp;
+      for (int l = 0; l <= 7; ++l) {
+        in = h;
+        if (l == 4) in.insert(in.end(), inp.begin(), inp.end());
+        else if (l != 0 && XA) in.insert(in.end(), xyz, xyz + 3);
+        if (l >= 1) {                                // the GEMM's packed columns
+          auto& m = sums[l];
+          if (l == 4) {
+            for (int c = 0; c < l3; ++c) m[c] += in[c];
+            for (int k = 0; k < 3; ++k) m[l3 + k] += xyz[k];
+          } else {
+            for (int c = 0; c < (int)in.size() && c < 512; ++c) m[c] += in[c];
+          }
+        }
+        a.assign(od[l], 0.f);
+        for (int r = 0; r < od[l]; ++r) {    // 8 partial sums: a vectorisable dot product
+          const float* wr = W[l] + (size_t)r * id[l];
+          float ps[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          int c = 0;
+          for (; c + 8 <= id[l]; c += 8)
+            for (int k = 0; k < 8; ++k) ps[k] += wr[c + k] * in[c + k];
+          float acc = B[l][r];
+          for (; c < id[l]; ++c) acc += wr[c] * in[c];
+          a[r] = acc + (((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7])));
+        }
+        ins[l] = in;
+        pre[l] = a;
+        if (LG[l]) {                                 // nn.LayerNorm(out_dim), eps 1e-5, biased variance
+          double mu = 0, var = 0;
+          for (float v : a) mu += v;
+          mu /= od[l];
+          for (float v : a) var += (v - mu) * (v - mu);
+          var /= od[l];
+          const double rs = 1.0 / std::sqrt(var + 1e-5);
+          for (int r = 0; r < od[l]; ++r) a[r] = (float)((a[r] - mu) * rs) * LG[l][r] + LB[l][r];
+        }
+        for (float& v : a) v = v > 0.f ? v : 0.f;
+        h = a;
+      }
+      if (gbar) {                                    // d sdf / d pre-activation, layer by layer down
+        float s8 = B[8][0];
+        for (int c = 0; c < id[8]; ++c) {
+          const float hv = c < (int)h.size() ? h[c] : xyz[c - (int)h.size()];   // (xyz_in_all: lin8 sees xyz too)
+          s8 += W[8][c] * hv;
+        }
+        float t = std::tanh(s8), y = t;
+        float g8 = 1.f - y * y;
+        if (use_tanh) { y = std::tanh(t); g8 = (1.f - y * y) * (1.f - t * t); }
+        std::vector<float> g(od[7]);
+        for (int r = 0; r < od[7]; ++r) g[r] = pre[7][r] > 0.f ? g8 * W[8][r] : 0.f;
+        for (int l = 7; l >= 0; --l) {
+          for (int r = 0; r < od[l]; ++r) gpart[th][l][r] += g[r];
+          if (l == 0) break;
+          std::vector<float> gi(od[l - 1], 0.f);     // W_l^T g, the h_{l-1} part, masked
+          for (int r = 0; r < od[l]; ++r) {
+            if (g[r] == 0.f) continue;
+            const float* wr = W[l] + (size_t)r * id[l];
+            for (int c = 0; c < od[l - 1]; ++c) gi[c] += wr[c] * g[r];
+          }
+          for (int c = 0; c < od[l - 1]; ++c) gi[c] = pre[l - 1][c] > 0.f ? gi[c] : 0.f;
+          g.swap(gi);
+        }
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nth; ++t) ts.emplace_back(work, t);
+  for (auto& t : ts) t.join();
+  std::vector<std::vector<double>> mean(8);
+  for (int l = 1; l <= 7; ++l) {
+    mean[l].assign(part[0][l].size(), 0.0);
+    for (int t = 0; t < nth; ++t)
+      for (size_t c = 0; c < mean[l].size(); ++c) mean[l][c] += part[t][l][c] / P;
+  }
+  if (gbar) {
+    gbar->assign(8, {});
+    for (int l = 0; l <= 7; ++l) {
+      (*gbar)[l].assign(512, 0.0);
+      for (int t = 0; t < nth; ++t)
+        for (int c = 0; c < 512; ++c) (*gbar)[l][c] += gpart[t][l][c] / P;
+    }
+  }
+  return mean;
+}
 
 int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, size_t n_floats,
                      dsr_decoder** out) {
@@ -502,14 +675,25 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   int Kf[8] = {0}, Kb[8] = {0};
   // split-fp16 forward fragments (stored as raw float storage in the same blob)
   int hf16[8] = {-1}, sw16[8] = {0};
+  // the forward packs' lo pieces by error feedback against each GEMM's mean input (pack_frag16)
+#ifndef DSR_EXP_NOFB
+  std::vector<std::vector<double>> gbar;           // (stays empty for LayerNorm decoders: to nearest)
+  const std::vector<std::vector<double>> hbar =
+      decoder_input_means(od, id, W, B, LG, LB, L, l3, XA, K4, d->use_tanh, d->norm_mask ? nullptr : &gbar);
+#else   // A/B: lo pieces to nearest
+  const std::vector<std::vector<double>> hbar(8);
+  std::vector<std::vector<double>> gbar;
+#endif
+  auto gb = [&](int l) { return (gbar.size() == 8 && !gbar[l].empty()) ? &gbar[l] : nullptr; };
   for (int l = 1; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 3) {
-      sw16[l] = pack_frag16(v16, 512, 512, A3);
+      sw16[l] = pack_frag16(v16, 512, 512, A3, hbar[l].empty() ? nullptr : &hbar[l]);
     } else if (l == 4) {
-      sw16[l] = pack_frag16(v16, 512, K4, A4);
+      sw16[l] = pack_frag16(v16, 512, K4, A4, hbar[l].empty() ? nullptr : &hbar[l]);
     } else {
-      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); });
+      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); },
+                            hbar[l].empty() ? nullptr : &hbar[l]);
     }
     std::vector<float> as_f((v16.size() + 1) / 2);
     std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
@@ -554,11 +738,11 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 0; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 0) {
-      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; });
+      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; }, gb(0));
     } else if (l == 3) {
-      swb16[l] = pack_frag16(v16, 512, K3b, [&](int r, int c) { return A3(c, r); });
+      swb16[l] = pack_frag16(v16, 512, K3b, [&](int r, int c) { return A3(c, r); }, gb(3));
     } else {
-      swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); });
+      swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); }, gb(l));
     }
     std::vector<float> as_f((v16.size() + 1) / 2);
     std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));

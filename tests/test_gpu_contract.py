@@ -233,7 +233,7 @@ def test_unperturbed_run_inside_the_reference_envelope(gpu_decoder):
         assert (g <= 2.0 * env).all(), (g, env)
 
 
-@pytest.mark.parametrize("name", ["kitti0"])
+@pytest.mark.parametrize("name", ["kitti0", "kitti5"])
 def test_ens256_distribution_per_iteration(gpu_decoder, name):
     """the metric object (F4 kitti0: KITTI params, 2048 pts x 2248 rays x 10
     iterations) from the 256 ulp-perturbed starts of the reference's golden F13 ensemble

@@ -15,8 +15,11 @@ from oracle import dsr_oracle as O  # noqa: E402
 from reconstruct.optimizer import sdf_eval  # noqa: E402
 
 os.environ["DSR_TEST_HOOKS"] = "1"
+import time  # noqa: E402
 state = S.make_decoder(1234)
+t0 = time.perf_counter()
 dec = decoder_from_state(state, S.DEFAULT_SPECS)
+print(f"decoder load {time.perf_counter() - t0:.3f} s (qualification {dec.info['probe_ms']:.1f} ms)", flush=True)
 layers = fold_state(state, S.DEFAULT_SPECS)
 o64 = O.Decoder(layers, dtype=np.float64)
 o32 = O.Decoder(layers)
@@ -40,6 +43,15 @@ for zs in (0.0, 0.05):
               f" J xyz mean {ej[:, 64:].mean():+.2e} rms {np.sqrt((ej[:, 64:] ** 2).mean()):.2e}"
               f" | sum_p J*e_sdf / sum|J||e| code {np.abs((j64[:, :64] * e[:, None]).sum(0)).max() / (np.abs(j64[:, :64]) * np.abs(e)[:, None]).sum(0).max():.3f}",
               flush=True)
+        # systematic part of the Jacobian error per component (its mean over points), RMS over the
+        # components, against the same for the random part — kink-flip points excluded
+        jr = np.abs(j.astype(np.float64) - j64).max(1) / np.abs(j64).max()
+        ok = jr < 1e-5
+        ejc = (j.astype(np.float64) - j64)[ok] / np.abs(j64[ok]).mean(0)
+        print(f"    J error per component (kinks excluded): systematic rms {np.sqrt((ejc.mean(0) ** 2).mean()):.2e}"
+              f" (code {np.sqrt((ejc[:, :64].mean(0) ** 2).mean()):.2e}, xyz {np.sqrt((ejc[:, 64:].mean(0) ** 2).mean()):.2e}),"
+              f" random rms {np.sqrt(ejc.var(0).mean()):.2e}", flush=True)
+        print(f"    J kink flips (per-point max |dJ| > 1e-5 max|J|): {np.mean(jr > 1e-5):.4f} of points; > 1e-6: {np.mean(jr > 1e-6):.4f}", flush=True)
         cbk = (np.arange(n) % 64) // 16          # the point's 16-point block in its 64-point tile
         print("    sdf mean by point block cb 0..3: " + " ".join(f"{e[cbk == k].mean():+.2e}" for k in range(4)), flush=True)
     stats("numpy fp32", y32, j32)
