@@ -16,7 +16,9 @@ config 4 (64 objects x 4096 points, 8 per GPU at N=8).
 Inputs are resident in HBM before the timed region (dsr_batch_create); each step
 re-initialises the optimizer state on device and runs all iterations.  At N=1 rank 0
 also reports: the exact-decode leg (``value_exact``: DSR_LITE=0, every ray sample
-decoded in 3xFP16), the three MFMA kernels' rooflines, the CPU baseline, the
+decoded in 3xFP16), the fp32-arithmetic leg (``fp32_leg``: the exact pass and the Jacobian
+on the fp32-MFMA kernels, their rates against the 157.3 TF fp32 MFMA peak), the three MFMA
+kernels' rooflines, the CPU baseline, the
 Redwood keyframe leg (BASELINE config 5, ``keyframe``), one 16-object KITTI frame as one batch
 (config 3 of the list, ``config2_frame``) and one object per ``reconstruct_object`` call
 (``config1_single``).
@@ -174,7 +176,8 @@ def stats_sum(acc, st):
             acc[k] = min(acc.get(k, 1e30), v)
         elif k in ("lite", "keep_masks", "surface_in_exact", "test_hooks", "lite_eligible", "audit",
                    "audit_shell", "audit_log2", "lite_margin0", "lite_floor", "lite_safety", "graph_captures",
-                   "graph_replays"):
+                   "graph_replays", "n_groups", "graph_mode", "fwd_variant", "jac_variant", "lite_variant",
+                   "split_ring"):
             acc[k] = v
         else:
             acc[k] = acc.get(k, 0) + v
@@ -191,6 +194,11 @@ def kernel_rooflines(a):
     out = {}
     split_peak, split_loop = FP16_MFMA_PEAK_TF / SPLIT_PRODUCTS, FP16_MFMA_LOOP_TF / SPLIT_PRODUCTS
     ren_mac = BWD_MAC if a.get("keep_masks") else FWD_MAC + BWD_MAC
+    # the fp32-MFMA kernels (DSR_FWD_VARIANT / DSR_JAC_VARIANT 0, the fp32 leg): fp32 products
+    # against the fp32 MFMA peak (no bare-loop figure for them: the spec stands in)
+    f32x, f32j = a.get("fwd_variant", 12) & 8 == 0, a.get("jac_variant", 12) & 8 == 0
+    xname, xpeak, xloop, xnote = (("k_mlp_fwd (fp32 MFMA)", FP32_MFMA_PEAK_TF, FP32_MFMA_PEAK_TF, "fp32 products")
+                                  if f32x else ("k_mlp_fwd16", split_peak, split_loop, "fp32-equivalent (3xFP16)"))
 
     def entry(name, flop, ms, launches, peak, loop, note):
         tf = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
@@ -204,13 +212,12 @@ def kernel_rooflines(a):
         entry("k_mlp_fwd_lite_st", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
               FP16_MFMA_PEAK_TF, FP16_MFMA_LOOP_TF, "2*1,769,984 per decoded ray sample, fp16 products")
         surf = a["jac_surface_points"] if a.get("surface_in_exact") else 0
-        entry("k_mlp_fwd16 (exact pass: band + audit samples" + (", surface points)" if surf else ")"),
-              2.0 * FWD_MAC * (a["refine_points"] + surf), a["refine_ms"], a["refine_launches"], split_peak,
-              split_loop, "2*1,769,984 per re-decoded sample" + (" and surface point" if surf else "")
-              + ", fp32-equivalent (3xFP16)")
+        entry(xname + " (exact pass: band + audit samples" + (", surface points)" if surf else ")"),
+              2.0 * FWD_MAC * (a["refine_points"] + surf), a["refine_ms"], a["refine_launches"], xpeak,
+              xloop, "2*1,769,984 per re-decoded sample" + (" and surface point" if surf else "") + ", " + xnote)
     else:
-        entry("k_mlp_fwd16", 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
-              split_peak, split_loop, "2*1,769,984 per decoded ray sample, fp32-equivalent (3xFP16)")
+        entry(xname, 2.0 * FWD_MAC * a["fwd_points"], a["fwd_ms"], a["fwd_launches"],
+              xpeak, xloop, "2*1,769,984 per decoded ray sample, " + xnote)
     if a.get("surface_in_exact"):      # every tile backward only (the exact pass ran the forwards)
         jflop = 2.0 * BWD_MAC * (a["jac_surface_points"] + a["jac_render_points"])
         note = "(N surface + K render points) x 2*1,835,520 (backward only, kept masks)"
@@ -218,7 +225,11 @@ def kernel_rooflines(a):
         jflop = 2.0 * (FWD_MAC + BWD_MAC) * a["jac_surface_points"] + 2.0 * ren_mac * a["jac_render_points"]
         note = ("N surface points x 2*(1,769,984+1,835,520) + K render points x 2*"
                 + ("1,835,520 (backward only, kept masks)" if a.get("keep_masks") else "(fwd+bwd)"))
-    entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop, note)
+    if f32j:
+        entry("k_mlp_jac (fp32 MFMA)", jflop, a["jac_ms"], a["jac_launches"], FP32_MFMA_PEAK_TF, FP32_MFMA_PEAK_TF,
+              note + ", fp32 products")
+    else:
+        entry("k_mlp_jac16", jflop, a["jac_ms"], a["jac_launches"], split_peak, split_loop, note)
     return out
 
 
@@ -662,6 +673,32 @@ def main():
         del os.environ["DSR_LITE"]
         out["value_exact"] = n_job * k / dt
         out["value_exact_note"] = "DSR_LITE=0: no classification pass, every in-ball sample decoded exactly"
+        # fp32-arithmetic leg: the same job with the exact pass and the
+        # Jacobian on the fp32-MFMA kernels (test hooks DSR_FWD_VARIANT / DSR_JAC_VARIANT 0; the
+        # lite classification stays fp16): what fp32 arithmetic costs, and those kernels' rate
+        # against the 157.3 TF fp32 MFMA peak
+        hooks = {"DSR_TEST_HOOKS": "1", "DSR_FWD_VARIANT": "0", "DSR_JAC_VARIANT": "0"}
+        os.environ.update(hooks)
+        f32 = ResidentShard(opt, objs)
+        f32.run()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(k):
+            f32.run()
+        dt = time.perf_counter() - t1
+        st32 = L.Stats()
+        ctx.check(lib.dsr_batch_stats(f32.handle, C.byref(st32)), "stats")
+        f32.close()
+        for key in hooks:
+            del os.environ[key]
+        a32 = stats_sum({}, st32)
+        out["fp32_leg"] = {"value": n_job * k / dt, "unit": "objects/s",
+                           "fwd_variant": a32.get("fwd_variant"), "jac_variant": a32.get("jac_variant"),
+                           "rooflines": {name: {k2: e[k2] for k2 in ("achieved_tflops", "peak_tflops", "frac_of_peak",
+                                                                     "avg_launch_ms", "launches")}
+                                         for name, e in kernel_rooflines(a32).items()},
+                           "note": "exact pass + Jacobian on v_mfma_f32_16x16x4_f32 (fp32 products), lite "
+                                   "classification unchanged; kernel rates over the last run's launches"}
         # the three MFMA kernels with the job on ONE stream: per-launch rates without the other
         # object group's concurrent kernels inside each launch's duration; the
         # headline roofline above is the timed region's, with both groups overlapping

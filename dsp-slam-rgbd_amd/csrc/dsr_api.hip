@@ -416,23 +416,30 @@ static _Float16 f16_other_side(_Float16 h, double r) {
   return o;
 }
 
+// Probe inputs of one split GEMM: P points' values of its input columns, in the GEMM's packed k
+// order, column-major (x[c * P + p]); empty: the pack's lo pieces round to nearest.
+struct ProbeCols {
+  std::vector<float> x;
+  int P = 0;
+  bool empty() const { return x.empty(); }
+};
+
 // Split-fp16 A fragments for v_mfma_f32_16x16x32_f16 (dsr_mlp16.hpp):
 // out[(((rb*T + t)*2 + piece)*64 + lane)*8 + j] = piece of src(16 rb + (lane&15), 32 t + 8 (lane>>4) + j) * 2^sw
-// hi = fp16(W 2^sw) and lo = one of the two fp16 neighbours of the remainder W 2^sw - hi.  With
-// `hbar` (the mean of each GEMM input column over a probe set, decoder_input_means) lo is chosen by
-// error feedback along each row — the neighbour that keeps sum_c (hi + lo - W 2^sw)_c hbar_c
-// closest to zero — instead of to nearest: hi + lo carries 22-23 of an fp32 weight's 24 bits, and
-// the rounded-away tails are a FIXED perturbation of the decoder, a smooth function of x that puts
-// the same offset on every nearby point's sdf (-2.3e-8 on the bench decoder, numpy emulation;
-// -2e-8 measured on the GPU, tools/bias_probe.py), which the sdf term's b = sum J r adds up.
-// Feedback rounding leaves each row's pre-activation offset at its mean input near zero (emulated:
-// -2.5e-9, a ninth).  Without hbar: round to nearest (the backward packs).
-// `tail` (non-null): also the third pieces fp16(W 2^sw - hi - lo) in the one-piece fragment layout
-// [rb][t][64 lanes] x 8 halfs (gemm16_tail): hi + lo + tail carries an fp32 weight exactly (tails
-// below the fp16 subnormals of weights ~2^-14 of the layer's largest excepted).
+// hi = fp16(W 2^sw) and lo = one of the two fp16 neighbours of the remainder W 2^sw - hi.  hi + lo
+// carries 22-23 of an fp32 weight's 24 bits, and the rounded-away tails are a FIXED perturbation
+// of the decoder: a smooth function of x that puts nearly the same error on every nearby point's
+// sdf and Jacobian, which b = sum_p J_p r_p adds up coherently (-2.3e-8 sdf offset and a 5e-8
+// Jacobian bias on the bench decoder with lo to nearest; numpy emulation and tools/bias_probe.py).
+// With `probe` (the GEMM's inputs at a fixed probe set, decoder_probe) lo is chosen by greedy error
+// feedback along each row: of the two neighbours, the one that keeps the row's error over the
+// probe points, sum_p ((hi + lo - W 2^sw) . x_p)^2, smallest — a GPTQ-style rounding against the
+// probe inputs' second moments, not only their mean.  Emulated on the bench decoder (/the sphere-
+// shell points of tools/bias_probe.py): Jacobian bias 5.0e-8 -> 1.2e-8 (mean-only feedback 2.1e-8),
+// random error 2.2e-7 -> 7.5e-8.  Rows are independent: split over a fixed 8 host threads, the
+// same packs on every host.
 static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
-                       const std::function<float(int, int)>& src, const std::vector<double>* hbar = nullptr,
-                       std::vector<_Float16>* tail = nullptr) {
+                       const std::function<float(int, int)>& src, const ProbeCols* probe = nullptr) {
   float mx = 0.f;
   for (int r = 0; r < rows_pad; ++r)
     for (int c = 0; c < cols_pad; ++c) mx = std::max(mx, std::fabs(src(r, c)));
@@ -441,57 +448,81 @@ static int pack_frag16(std::vector<_Float16>& out, int rows_pad, int cols_pad,
   const int sw = 14 - e;                            // max |W| * 2^sw < 2^14
   const int RB = rows_pad / 16, T = cols_pad / 32;
   out.assign((size_t)RB * T * 2 * 64 * 8, (_Float16)0.f);
-  if (tail) tail->assign((size_t)RB * T * 64 * 8, (_Float16)0.f);
-  std::vector<_Float16> hi((size_t)cols_pad), lo((size_t)cols_pad), tl((size_t)cols_pad);
-  for (int r = 0; r < rows_pad; ++r) {
-    double acc = 0.0;                               // the row's running sum of (hi + lo - x) hbar
-    for (int c = 0; c < cols_pad; ++c) {
-      const float x = std::ldexp(src(r, c), sw);
-      const _Float16 h = (_Float16)x;
-      const double rem = (double)x - (double)(float)h;   // exact
-      _Float16 l = (_Float16)(float)rem;                 // to nearest (rem is exact in fp32)
-      if (hbar && (double)(float)l != rem) {
-        const _Float16 l2 = f16_other_side(l, rem);
-        const double w = (*hbar)[c];
-        const double e1 = acc + ((double)(float)l - rem) * w, e2 = acc + ((double)(float)l2 - rem) * w;
-        if (std::fabs(e2) < std::fabs(e1)) l = l2;
-      }
-      acc += ((double)(float)l - rem) * (hbar ? (*hbar)[c] : 0.0);
-      hi[c] = h;
-      lo[c] = l;
-      tl[c] = (_Float16)(float)(rem - (double)(float)l);   // exact difference, rounded once
-    }
-    const int rb = r >> 4, lr = r & 15;
-    // odd 16-row blocks negated (SPLIT_ROW_SIGNS, dsr_mlp16.hpp: row_sign): exact, both pieces
-    const bool neg = SPLIT_ROW_SIGNS && (rb & 1);
-    for (int t = 0; t < T; ++t)
-      for (int g = 0; g < 4; ++g)
-        for (int j = 0; j < 8; ++j) {
-          const int c = 32 * t + 8 * g + j, lane = lr + 16 * g;
-          out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = neg ? (_Float16)(-hi[c]) : hi[c];
-          out[((((size_t)rb * T + t) * 2 + 1) * 64 + lane) * 8 + j] = neg ? (_Float16)(-lo[c]) : lo[c];
-          if (tail) (*tail)[(((size_t)rb * T + t) * 64 + lane) * 8 + j] = neg ? (_Float16)(-tl[c]) : tl[c];
+  const bool fb = probe && !probe->empty() && probe->x.size() == (size_t)cols_pad * probe->P;
+  const int P = fb ? probe->P : 0;
+  const float* X = fb ? probe->x.data() : nullptr;
+  std::vector<double> nrm((size_t)cols_pad, 0.0);   // |x_c|^2 over the probe points
+  for (int c = 0; fb && c < cols_pad; ++c)
+    for (int p = 0; p < P; ++p) nrm[c] += (double)X[(size_t)c * P + p] * X[(size_t)c * P + p];
+  auto rows = [&](int th, int nth) {
+    std::vector<_Float16> hi((size_t)cols_pad), lo((size_t)cols_pad);
+    std::vector<double> u((size_t)P);               // the row's error at each probe point so far
+    for (int r = th; r < rows_pad; r += nth) {
+      std::fill(u.begin(), u.end(), 0.0);
+      for (int c = 0; c < cols_pad; ++c) {
+        const float x = std::ldexp(src(r, c), sw);
+        const _Float16 h = (_Float16)x;
+        const double rem = (double)x - (double)(float)h;   // exact
+        _Float16 l = (_Float16)(float)rem;                 // to nearest (rem is exact in fp32)
+        bool upd = false;
+        if (fb && nrm[c] > 0.0 && (double)(float)l != rem) {
+          const float* xs = X + (size_t)c * P;
+          double dot = 0.0;
+          for (int p = 0; p < P; ++p) dot += u[p] * xs[p];
+          const _Float16 l2 = f16_other_side(l, rem);
+          const double d1 = (double)(float)l - rem, d2 = (double)(float)l2 - rem;
+          if (2.0 * d2 * dot + d2 * d2 * nrm[c] < 2.0 * d1 * dot + d1 * d1 * nrm[c]) l = l2;
+          upd = true;
         }
+        if (upd) {
+          const double d = (double)(float)l - rem;
+          const float* xs = X + (size_t)c * P;
+          for (int p = 0; p < P; ++p) u[p] += d * xs[p];
+        }
+        hi[c] = h;
+        lo[c] = l;
+      }
+      const int rb = r >> 4, lr = r & 15;
+      // odd 16-row blocks negated (SPLIT_ROW_SIGNS, dsr_mlp16.hpp: row_sign): exact, both pieces
+      const bool neg = SPLIT_ROW_SIGNS && (rb & 1);
+      for (int t = 0; t < T; ++t)
+        for (int g = 0; g < 4; ++g)
+          for (int j = 0; j < 8; ++j) {
+            const int c = 32 * t + 8 * g + j, lane = lr + 16 * g;
+            out[((((size_t)rb * T + t) * 2 + 0) * 64 + lane) * 8 + j] = neg ? (_Float16)(-hi[c]) : hi[c];
+            out[((((size_t)rb * T + t) * 2 + 1) * 64 + lane) * 8 + j] = neg ? (_Float16)(-lo[c]) : lo[c];
+          }
+    }
+  };
+  if (!fb) {
+    rows(0, 1);
+  } else {
+    constexpr int nth = 8;
+    std::vector<std::thread> ts;
+    for (int t = 0; t < nth; ++t) ts.emplace_back(rows, t, nth);
+    for (auto& t : ts) t.join();
   }
   return sw;
 }
 
 static int decoder_qualify(dsr_ctx* ctx, dsr_decoder* dec);
 
-// Mean input of each split forward GEMM (lin1..lin7) over a fixed probe set — 256 points uniform
-// in the unit ball (fixed LCG), code 0 — in the packed column order pack_frag16 uses: lin l's
-// columns are its input h_{l-1} (with xyz at 509..511 under xyz_in_all); lin4's are h3 (l3) then
-// xyz (the code is folded into its bias).  A host forward pass of deep_sdf_decoder.py:75-110 in
-// fp32 (LayerNorm and xyz_in_all included), split over host threads; ~0.1 s once per load.
-// With `gbar` (non-null, decoders without LayerNorm): also the mean of d sdf / d(pre-activation of
-// lin l) (masked by its ReLU) for l = 0..7 — the input of the backward GEMM W_l^T, in its packed
-// column order (lin l's outputs) — for the backward packs' feedback rounding.
-static std::vector<std::vector<double>> decoder_input_means(const int* od, const int* id, const std::vector<const float*>& W,
-                                                            const std::vector<const float*>& B,
-                                                            const std::vector<const float*>& LG,
-                                                            const std::vector<const float*>& LB, int L, int l3, int XA,
-                                                            int K4, int use_tanh = 0,
-                                                            std::vector<std::vector<double>>* gbar = nullptr) {
+// The split GEMMs' inputs at a fixed probe set — 256 points uniform in the unit ball (fixed LCG),
+// code 0 — in the packed column order pack_frag16 uses, for its feedback rounding:
+//  fwd[l], l = 1..7: lin l's input h_{l-1} (with xyz at 509..511 under xyz_in_all); lin4's columns
+//    are h3 (l3) then xyz (the code is folded into its bias);
+//  bwd[l], l = 0..7: d sdf / d(output of lin l), through its ReLU (and LayerNorm, if any) — the
+//    input of the backward GEMM W_l^T, over lin l's outputs.
+// A host forward + backward pass of deep_sdf_decoder.py:75-110 in fp32 (LayerNorm, use_tanh and
+// xyz_in_all included), split over a fixed 8 host threads (not the core count: the same probes,
+// hence the same packs, on every host); well under 0.1 s once per load.
+struct DecoderProbe {
+  ProbeCols fwd[8], bwd[8];
+};
+static DecoderProbe decoder_probe(const int* od, const int* id, const std::vector<const float*>& W,
+                                  const std::vector<const float*>& B, const std::vector<const float*>& LG,
+                                  const std::vector<const float*>& LB, int L, int l3, int XA, int K4, int K3b,
+                                  int use_tanh, bool with_bwd) {
   constexpr int P = 256;
   std::vector<float> pts((size_t)P * 3);
   uint64_t s = 0xD1B54A32D192ED03ull;
@@ -505,15 +536,21 @@ static std::vector<std::vector<double>> decoder_input_means(const int* od, const
     pts[3 * i] = (float)x; pts[3 * i + 1] = (float)y; pts[3 * i + 2] = (float)z;
     ++i;
   }
-  constexpr int nth = 8;      // fixed (not the host's core count): the means, hence the packs, are the same on every host
-  std::vector<std::vector<std::vector<double>>> part(nth, std::vector<std::vector<double>>(8));
-  std::vector<std::vector<std::vector<double>>> gpart(nth, std::vector<std::vector<double>>(8));
-  auto work = [&](int th) {
-    auto& sums = part[th];
-    for (int l = 1; l <= 7; ++l) sums[l].assign(l == 4 ? K4 : 512, 0.0);
-    for (int l = 0; l <= 7; ++l) gpart[th][l].assign(512, 0.0);
+  DecoderProbe pr;
+  for (int l = 0; l <= 7; ++l) {
+    if (l >= 1) {
+      pr.fwd[l].P = P;
+      pr.fwd[l].x.assign((size_t)(l == 4 ? K4 : 512) * P, 0.f);
+    }
+    if (with_bwd) {
+      pr.bwd[l].P = P;
+      pr.bwd[l].x.assign((size_t)(l == 3 ? K3b : 512) * P, 0.f);
+    }
+  }
+  auto work = [&](int th, int nth) {
     std::vector<float> h, in, a;
-    std::vector<std::vector<float>> ins(9), pre(9);
+    std::vector<std::vector<float>> post(9), xh(9);   // pre-ReLU values (after LayerNorm); x^
+    std::vector<double> rs(9, 0.0);                    // LayerNorm 1 / sqrt(var + eps)
     for (int p = th; p < P; p += nth) {
       const float* xyz = &pts[3 * p];
       std::vector<float> inp((size_t)L + 3, 0.f);  // [code (0) | xyz]
@@ -524,12 +561,12 @@ static std::vector<std::vector<double>> decoder_input_means(const int* od, const
         if (l == 4) in.insert(in.end(), inp.begin(), inp.end());
         else if (l != 0 && XA) in.insert(in.end(), xyz, xyz + 3);
         if (l >= 1) {                                // the GEMM's packed columns
-          auto& m = sums[l];
+          float* m = pr.fwd[l].x.data();
           if (l == 4) {
-            for (int c = 0; c < l3; ++c) m[c] += in[c];
-            for (int k = 0; k < 3; ++k) m[l3 + k] += xyz[k];
+            for (int c = 0; c < l3; ++c) m[(size_t)c * P + p] = in[c];
+            for (int k = 0; k < 3; ++k) m[(size_t)(l3 + k) * P + p] = xyz[k];
           } else {
-            for (int c = 0; c < (int)in.size() && c < 512; ++c) m[c] += in[c];
+            for (int c = 0; c < (int)in.size() && c < 512; ++c) m[(size_t)c * P + p] = in[c];
           }
         }
         a.assign(od[l], 0.f);
@@ -543,64 +580,67 @@ static std::vector<std::vector<double>> decoder_input_means(const int* od, const
           for (; c < id[l]; ++c) acc += wr[c] * in[c];
           a[r] = acc + (((ps[0] + ps[1]) + (ps[2] + ps[3])) + ((ps[4] + ps[5]) + (ps[6] + ps[7])));
         }
-        ins[l] = in;
-        pre[l] = a;
         if (LG[l]) {                                 // nn.LayerNorm(out_dim), eps 1e-5, biased variance
           double mu = 0, var = 0;
           for (float v : a) mu += v;
           mu /= od[l];
           for (float v : a) var += (v - mu) * (v - mu);
           var /= od[l];
-          const double rs = 1.0 / std::sqrt(var + 1e-5);
-          for (int r = 0; r < od[l]; ++r) a[r] = (float)((a[r] - mu) * rs) * LG[l][r] + LB[l][r];
+          rs[l] = 1.0 / std::sqrt(var + 1e-5);
+          xh[l].resize(od[l]);
+          for (int r = 0; r < od[l]; ++r) {
+            xh[l][r] = (float)((a[r] - mu) * rs[l]);
+            a[r] = xh[l][r] * LG[l][r] + LB[l][r];
+          }
         }
+        post[l] = a;
         for (float& v : a) v = v > 0.f ? v : 0.f;
         h = a;
       }
-      if (gbar) {                                    // d sdf / d pre-activation, layer by layer down
-        float s8 = B[8][0];
-        for (int c = 0; c < id[8]; ++c) {
-          const float hv = c < (int)h.size() ? h[c] : xyz[c - (int)h.size()];   // (xyz_in_all: lin8 sees xyz too)
-          s8 += W[8][c] * hv;
-        }
-        float t = std::tanh(s8), y = t;
-        float g8 = 1.f - y * y;
-        if (use_tanh) { y = std::tanh(t); g8 = (1.f - y * y) * (1.f - t * t); }
-        std::vector<float> g(od[7]);
-        for (int r = 0; r < od[7]; ++r) g[r] = pre[7][r] > 0.f ? g8 * W[8][r] : 0.f;
-        for (int l = 7; l >= 0; --l) {
-          for (int r = 0; r < od[l]; ++r) gpart[th][l][r] += g[r];
-          if (l == 0) break;
-          std::vector<float> gi(od[l - 1], 0.f);     // W_l^T g, the h_{l-1} part, masked
+      if (!with_bwd) continue;
+      // d sdf / d pre-activation, layer by layer down
+      float s8 = B[8][0];
+      for (int c = 0; c < id[8]; ++c) {
+        const float hv = c < (int)h.size() ? h[c] : xyz[c - (int)h.size()];   // (xyz_in_all: lin8 sees xyz too)
+        s8 += W[8][c] * hv;
+      }
+      float t = std::tanh(s8), y = t;
+      float g8 = 1.f - y * y;
+      if (use_tanh) { y = std::tanh(t); g8 = (1.f - y * y) * (1.f - t * t); }
+      std::vector<float> g(od[7]);
+      for (int r = 0; r < od[7]; ++r) g[r] = post[7][r] > 0.f ? g8 * W[8][r] : 0.f;
+      for (int l = 7; l >= 0; --l) {
+        if (LG[l]) {                                 // through the LayerNorm (dsr_oracle.forward_jac)
+          double m1 = 0, m2 = 0;
           for (int r = 0; r < od[l]; ++r) {
-            if (g[r] == 0.f) continue;
-            const float* wr = W[l] + (size_t)r * id[l];
-            for (int c = 0; c < od[l - 1]; ++c) gi[c] += wr[c] * g[r];
+            const double gx = (double)g[r] * LG[l][r];
+            m1 += gx;
+            m2 += gx * xh[l][r];
           }
-          for (int c = 0; c < od[l - 1]; ++c) gi[c] = pre[l - 1][c] > 0.f ? gi[c] : 0.f;
-          g.swap(gi);
+          m1 /= od[l];
+          m2 /= od[l];
+          for (int r = 0; r < od[l]; ++r)
+            g[r] = (float)(rs[l] * ((double)g[r] * LG[l][r] - m1 - xh[l][r] * m2));
         }
+        float* m = pr.bwd[l].x.data();
+        for (int r = 0; r < od[l]; ++r) m[(size_t)r * P + p] = g[r];
+        if (l == 0) break;
+        std::vector<float> gi(od[l - 1], 0.f);     // W_l^T g, the h_{l-1} part, masked
+        for (int r = 0; r < od[l]; ++r) {
+          if (g[r] == 0.f) continue;
+          const float* wr = W[l] + (size_t)r * id[l];
+          for (int c = 0; c < od[l - 1]; ++c) gi[c] += wr[c] * g[r];
+        }
+        for (int c = 0; c < od[l - 1]; ++c) gi[c] = post[l - 1][c] > 0.f ? gi[c] : 0.f;
+        g.swap(gi);
       }
     }
   };
+  constexpr int nth = 8;
   std::vector<std::thread> ts;
-  for (int t = 0; t < nth; ++t) ts.emplace_back(work, t);
+  for (int t = 0; t < nth; ++t) ts.emplace_back(work, t, nth);
   for (auto& t : ts) t.join();
-  std::vector<std::vector<double>> mean(8);
-  for (int l = 1; l <= 7; ++l) {
-    mean[l].assign(part[0][l].size(), 0.0);
-    for (int t = 0; t < nth; ++t)
-      for (size_t c = 0; c < mean[l].size(); ++c) mean[l][c] += part[t][l][c] / P;
-  }
-  if (gbar) {
-    gbar->assign(8, {});
-    for (int l = 0; l <= 7; ++l) {
-      (*gbar)[l].assign(512, 0.0);
-      for (int t = 0; t < nth; ++t)
-        for (int c = 0; c < 512; ++c) (*gbar)[l][c] += gpart[t][l][c] / P;
-    }
-  }
-  return mean;
+  return pr;
 }
 
 int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, size_t n_floats,
@@ -656,7 +696,7 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   // is folded into the per-object bias.
   // (the GEMM k loops are unrolled for 14 or 16 k steps: lin4's h3 | xyz depth and lin3^T's depth
   // pad to 448 or 512 — zero weights over the ReLU'd zero rows of lin3's padded outputs)
-  const int K4 = l3 + 3 <= 448 ? 448 : 512, K3b = l3 <= 448 ? 448 : 512;
+  const int K4 = l3 + 3 <= 448 ? 448 : 512;
   auto E0 = [&](int r, int c) {            // lin0 in the 64-D layout: [code (64) | xyz (3)]
     return c < CODE ? (c < L ? Wat(0, r, c) : 0.f) : Wat(0, r, L + (c - CODE));
   };
@@ -675,25 +715,21 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   int Kf[8] = {0}, Kb[8] = {0};
   // split-fp16 forward fragments (stored as raw float storage in the same blob)
   int hf16[8] = {-1}, sw16[8] = {0};
-  // the forward packs' lo pieces by error feedback against each GEMM's mean input (pack_frag16)
+  // the packs' lo pieces by error feedback against each GEMM's inputs at a probe set (pack_frag16)
+  const int K3b = l3 <= 448 ? 448 : 512;
 #ifndef DSR_EXP_NOFB
-  std::vector<std::vector<double>> gbar;           // (stays empty for LayerNorm decoders: to nearest)
-  const std::vector<std::vector<double>> hbar =
-      decoder_input_means(od, id, W, B, LG, LB, L, l3, XA, K4, d->use_tanh, d->norm_mask ? nullptr : &gbar);
+  const DecoderProbe probe = decoder_probe(od, id, W, B, LG, LB, L, l3, XA, K4, K3b, d->use_tanh, true);
 #else   // A/B: lo pieces to nearest
-  const std::vector<std::vector<double>> hbar(8);
-  std::vector<std::vector<double>> gbar;
+  const DecoderProbe probe;
 #endif
-  auto gb = [&](int l) { return (gbar.size() == 8 && !gbar[l].empty()) ? &gbar[l] : nullptr; };
   for (int l = 1; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 3) {
-      sw16[l] = pack_frag16(v16, 512, 512, A3, hbar[l].empty() ? nullptr : &hbar[l]);
+      sw16[l] = pack_frag16(v16, 512, 512, A3, &probe.fwd[l]);
     } else if (l == 4) {
-      sw16[l] = pack_frag16(v16, 512, K4, A4, hbar[l].empty() ? nullptr : &hbar[l]);
+      sw16[l] = pack_frag16(v16, 512, K4, A4, &probe.fwd[l]);
     } else {
-      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); },
-                            hbar[l].empty() ? nullptr : &hbar[l]);
+      sw16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, r, c); }, &probe.fwd[l]);
     }
     std::vector<float> as_f((v16.size() + 1) / 2);
     std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));
@@ -738,11 +774,11 @@ int dsr_decoder_load(dsr_ctx* ctx, const dsr_decoder_desc* d, const float* w, si
   for (int l = 0; l <= 7; ++l) {
     std::vector<_Float16> v16;
     if (l == 0) {
-      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; }, gb(0));
+      swb16[l] = pack_frag16(v16, 80, 512, [&](int r, int c) { return r < IN ? E0(c, r) : 0.f; }, &probe.bwd[0]);
     } else if (l == 3) {
-      swb16[l] = pack_frag16(v16, 512, K3b, [&](int r, int c) { return A3(c, r); }, gb(3));
+      swb16[l] = pack_frag16(v16, 512, K3b, [&](int r, int c) { return A3(c, r); }, &probe.bwd[3]);
     } else {
-      swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); }, gb(l));
+      swb16[l] = pack_frag16(v16, 512, 512, [&](int r, int c) { return Wat(l, c, r); }, &probe.bwd[l]);
     }
     std::vector<float> as_f((v16.size() + 1) / 2);
     std::memcpy(as_f.data(), v16.data(), v16.size() * sizeof(_Float16));

@@ -1198,6 +1198,17 @@ struct Jac16Shared {
   float wmax[NWAVE];
 };
 
+// The backward GEMMs (W_l^T) chain their lo products from zero (gemm16_sel's LS, dsr_mlp16.hpp),
+// as the forward ones do: the Jacobian's own rounding bias then no longer dominates its error
+// (tools/bias_probe.py: J bias 3.4e-8 -> 2.3e-8 of |J|, random 8.3e-7 -> 5.8e-7; fp32 numpy
+// 5.7e-9 / 7.2e-7) — the sum b = sum_p J_p r_p cancels to ~1e-5 of its terms on a converging
+// object, so that bias, not the random error, is what its pose rows see.
+#ifdef DSR_EXP_NOLS
+constexpr int BWD_LS = 0;
+#else
+constexpr int BWD_LS = 1;
+#endif
+
 // NB: A ring depth of the split GEMMs (gemm16_sel; 0 = the two-set gemm16_tile).  Lane-derived
 // values are re-derived per layer from an opaque lane id (dsr_mlp_lite.hpp, "Register
 // discipline"); row-selecting conditions are wave-uniform branches + per-lane selects.
@@ -1364,7 +1375,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll 1
       for (int l = 1; l <= 6; ++l) {
         const int lane = opaque(threadIdx.x & 63), g = lane >> 4;
-        gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
+        gemm16_sel<PRIO, NB, JFWD_LS>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
         JSTAMP(1)
         const float usc = ldexpf(1.f, -(D.sw[l] + fs.b));
         const float* bias = (l == 4) ? bias4f + tl.obj * HID : D.bias[l];
@@ -1423,7 +1434,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
       // ---- lin7 + lin8 dot + tanh
       {
         const int lane = opaque(threadIdx.x & 63);
-        gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
+        gemm16_sel<PRIO, NB, JFWD_LS>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, fs.resc());
         JSTAMP(1)
         const int un = D.sw[7] + fs.b;
 #pragma unroll
@@ -1493,7 +1504,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
 #pragma unroll 1
     for (int l = 7; l >= 1; --l) {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
-      gemm16_sel<PRIO, NB>(D.Wbh_raw[l], w, D.Kb[l] / 32, sm.Hh, sm.Hl, acc, lane);
+      gemm16_sel<PRIO, NB, BWD_LS>(D.Wbh_raw[l], w, D.Kb[l] / 32, sm.Hh, sm.Hl, acc, lane);
       JSTAMP(1)
       const float usc = ldexpf(1.f, -(D.swb[l] + sa));
       float m = 0.f;
@@ -1557,7 +1568,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     if (w < 5) {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       floatx4 a1[1][4];
-      gemm16_tile<PRIO, 1>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
+      gemm16_tile<PRIO, 1, 0, BWD_LS>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
                            sm.Hh, sm.Hl, a1, lane);
       const int un = D.swb[0] + sa;
 #pragma unroll

@@ -53,16 +53,17 @@ constexpr bool SPLIT_ROW_SIGNS = true;
 // 80-row pack, whose wave w owns rows 16w .. 16w + 15, pass w
 __device__ __forceinline__ constexpr float row_sign(int q) { return (SPLIT_ROW_SIGNS && (q & 1)) ? -1.f : 1.f; }
 // Row signs alone leave each point's sdf off by eps * (S_even - S_odd) (the two row halves' shares
-// of lin8's sum), -2e-8 on the bench decoder.  The activation images carry a column sign as well:
-// write_split stores the points of odd 16-point blocks cb (points 16cb .. 16cb + 15) negated, so
-// those output columns accumulate -(W h) too and element (q, cb) leans with row_sign(q) *
-// col_sign(cb) — a checkerboard: a point's remaining lean has the sign of its column block, and
-// sums over points (b, the losses) see no common offset.  The epilogues undo the sign with the
-// same exact multiply.
-#ifdef DSR_EXP_ROWONLY   // A/B: row signs only
-__device__ __forceinline__ constexpr float col_sign(int) { return 1.f; }
-#else
+// of lin8's sum), -2e-8 on the bench decoder, with lo products chained onto the running sum.
+// Chained from zero instead (LS below) the lean is gone (+2e-9, tools/bias_probe.py).  A column
+// sign as well (odd 16-point blocks negated: a checkerboard, measured in round 5) cancelled that
+// lean over points, but made a point's result depend on its slot in the tile — the lite pass's
+// band re-decode, a re-run from a saved state and an 8-rank shard then disagreed with the exact
+// pass in the last bits (test_gpu_parity.py's bitwise checks) — so it is not built;
+// DSR_EXP_COLSIGN (A/B) restores it.
+#ifdef DSR_EXP_COLSIGN
 __device__ __forceinline__ constexpr float col_sign(int cb) { return (SPLIT_ROW_SIGNS && (cb & 1)) ? -1.f : 1.f; }
+#else
+__device__ __forceinline__ constexpr float col_sign(int) { return 1.f; }
 #endif
 __device__ __forceinline__ constexpr float rc_sign(int q, int cb) { return row_sign(q) * col_sign(cb); }
 
@@ -86,10 +87,36 @@ __device__ __forceinline__ int h_boff(int lane) {
   return c * PH + 8 * ((lane >> 4) ^ ((c >> 2) & 1));
 }
 
-template <bool PRIO, int NQ, int EX = 0>
+// LS (every split GEMM): each k step's two lo products chained from zero and added to the
+// running sum on the VALU (round to nearest) instead of onto it in the MFMA.
+// The f16 MFMA rounds each 8-deep chunk sum onto its accumulator toward -inf to about an ulp of
+// the ACCUMULATOR (tools/mfma_numerics.py): chained onto the large running sum, the two small lo
+// products cost two such roundings per k step for ~2^-11 of the product's value; from zero they
+// round to their own size.  Measured on one decoder-layer-shaped block (tools/split_chain_bias.py):
+// mean error -1.36e-8 -> -1.6e-9 of |exact|, rms 2.4e-7 -> 1.6e-7.
+template <bool PRIO, int NQ, int EX = 0, bool LS = false>
 __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&al)[NQ], const half8 (&bh)[4],
                                            const half8 (&bl)[4], floatx4 (&acc)[NQ][4]) {
   if (PRIO) __builtin_amdgcn_s_setprio(1);
+  if constexpr (LS && (EX & 1) == 0) {
+    // per column block: the NQ lo chains side by side, the hi products onto the running sums,
+    // then the VALU adds of the lo sums (adding them before the hi product instead is the same
+    // arithmetic in another order; measured no faster)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      floatx4 lo[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        lo[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[q], bh[cb], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) lo[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bl[cb], lo[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[q], bh[cb], acc[q][cb], 0, 0, 0) + lo[q];
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    return;
+  }
   if constexpr ((EX & 1) == 0) {       // EX bit0: timing experiment, hi.hi product only
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -190,7 +217,7 @@ __device__ __forceinline__ void rescale_acc(floatx4 (&acc)[NQ][4], float f) {
     for (int cb = 0; cb < 4; ++cb) acc[q][cb] = acc[q][cb] * f;
 }
 
-template <bool PRIO, int NQ = 4, int EX = 0>
+template <bool PRIO, int NQ = 4, int EX = 0, bool LS = false>
 __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, const _Float16* Hh,
                                             const _Float16* Hl, floatx4 (&acc)[NQ][4], int lane,
                                             float resc = 1.f) {
@@ -221,7 +248,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
       bl1[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * (t + 1));
     }
     if (t == 8 && resc != 1.f) rescale_acc<NQ>(acc, resc);
-    mfma3_step<PRIO, NQ, EX>(ah0, al0, bh0, bl0, acc);
+    mfma3_step<PRIO, NQ, EX, LS>(ah0, al0, bh0, bl0, acc);
     const int tn = (t + 2 < T) ? t + 2 : T - 1;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -233,7 +260,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
       bh0[cb] = *reinterpret_cast<const half8*>(Bh + cb * 16 * PH + 32 * tn);
       bl0[cb] = *reinterpret_cast<const half8*>(Bl + cb * 16 * PH + 32 * tn);
     }
-    mfma3_step<PRIO, NQ, EX>(ah1, al1, bh1, bl1, acc);
+    mfma3_step<PRIO, NQ, EX, LS>(ah1, al1, bh1, bl1, acc);
   }
 }
 
@@ -243,7 +270,7 @@ __device__ __forceinline__ void gemm16_tile(const half8* __restrict__ A, int T, 
 // read from LDS as the current block's MFMAs issue, and the three products of an accumulator
 // issued back to back in mfma3_step's order (al.bh, ah.bl, ah.bh) — so the sums are bitwise
 // those of gemm16_tile.  The first step starts from an inline zero C operand.
-template <bool PRIO, int T, int NB>
+template <bool PRIO, int T, int NB, int LS = 0>
 __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Float16* Hh, const _Float16* Hl,
                                             floatx4 (&acc)[4][4], int lane, float resc) {
   const _Float16* base = Wl + (size_t)(4 * w) * T * 2 * 64 * 8;
@@ -261,6 +288,11 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
         half8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, ((q * T + t) * 2 + piece) * 1024, 0));
   };
   half8 ah[NB][4], al[NB][4], bh[2], bl[2];
+  floatx4 lacc[4][4];                  // LS 2: the lo products' own accumulators
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) lacc[q][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NB - 1; ++j)
 #pragma unroll
@@ -279,7 +311,10 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
         al[(j + NB - 1) % NB][q] = lda(q, t + NB - 1, 1);
       }
     }
-    if (!decltype(FIRST)::value && t == 8 && resc != 1.f) rescale_acc<4>(acc, resc);
+    if (!decltype(FIRST)::value && t == 8 && resc != 1.f) {
+      rescale_acc<4>(acc, resc);
+      if constexpr (LS == 2) rescale_acc<4>(lacc, resc);
+    }
     if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -296,11 +331,32 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         floatx4 x = decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb];
+        if constexpr (LS == 2) {
+          lacc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[j][q], bh[cb & 1], lacc[q][cb], 0, 0, 0);
+          lacc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bl[cb & 1], lacc[q][cb], 0, 0, 0);
+          acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bh[cb & 1], x, 0, 0, 0);
+          continue;
+        }
+        if constexpr (LS == 1) continue;         // below, the block's four q at once
 #ifndef DSR_EXP_ONEPROD            // timing experiment (invalid results): the hi.hi product only
         x = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[j][q], bh[cb & 1], x, 0, 0, 0);
         x = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bl[cb & 1], x, 0, 0, 0);
 #endif
         acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bh[cb & 1], x, 0, 0, 0);
+      }
+      if constexpr (LS == 1) {
+        // the four lo chains side by side, the hi products onto the running sums, then the VALU
+        // adds of the lo sums
+        floatx4 lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          lo[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[j][q], bh[cb & 1], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lo[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[j][q], bl[cb & 1], lo[q], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[q][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              ah[j][q], bh[cb & 1], decltype(FIRST)::value ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[q][cb], 0, 0, 0) + lo[q];
       }
     }
     if (PRIO) __builtin_amdgcn_s_setprio(0);
@@ -316,23 +372,53 @@ __device__ __forceinline__ void gemm16_ring(const _Float16* Wl, int w, const _Fl
   [&]<int... J>(std::integer_sequence<int, J...>) {
     (step(std::integral_constant<int, (TM + J) % NB>{}, std::false_type{}, TM + J), ...);
   }(std::make_integer_sequence<int, T - TM>{});
+  if constexpr (LS == 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[q][cb] += lacc[q][cb];
+  }
 }
 
 // acc = split product of the wave's 64 rows of packed matrix Wl (K = 32 T, T 16 or 14) and
 // the 64-point image: ring schedule with NB k steps in flight (NB 0: gemm16_tile).  `resc`
 // (a power of two) moves the partial sums from the image's group-A scale to its group-B
 // scale before k step 8 (Scales2); 1 for an image under one scale.
-template <bool PRIO, int NB>
+template <bool PRIO, int NB, int LS = 0>
 __device__ __forceinline__ void gemm16_sel(const _Float16* Wl, int w, int T, const _Float16* Hh,
                                            const _Float16* Hl, floatx4 (&acc)[4][4], int lane,
                                            float resc = 1.f) {
   if constexpr (NB == 0) {
-    gemm16_tile<PRIO, 4>(wfrag(Wl, w, T), T, Hh, Hl, acc, lane, resc);
+    gemm16_tile<PRIO, 4, 0, (LS != 0)>(wfrag(Wl, w, T), T, Hh, Hl, acc, lane, resc);
   } else {
-    if (T != 14) gemm16_ring<PRIO, 16, NB>(Wl, w, Hh, Hl, acc, lane, resc);
-    else gemm16_ring<PRIO, 14, NB>(Wl, w, Hh, Hl, acc, lane, resc);
+    if (T != 14) gemm16_ring<PRIO, 16, NB, LS>(Wl, w, Hh, Hl, acc, lane, resc);
+    else gemm16_ring<PRIO, 14, NB, LS>(Wl, w, Hh, Hl, acc, lane, resc);
   }
 }
+
+// Every split GEMM chains its lo products per k step from zero (LS 1).  The exact pass could
+// keep them in their own accumulators over the whole k loop instead (LS 2: 64 more VGPRs, which
+// k_mlp_fwd16 has to spare, one VALU add per output; DSR_EXP_FLS2) and the bench gained ~2%, but
+// the Jacobian kernel has no VGPRs to spare for it, and a sample's masks and sdf must be the same
+// bits whichever kernel computes them (test_gpu_parity.py: the lite pass against the exact
+// decode, the broken-block fallback; test_gpu_bench.py: 8-rank shards against one rank).
+#ifdef DSR_EXP_JFLS0
+constexpr int JFWD_LS = 0;
+#else
+constexpr int JFWD_LS = 1;
+#endif
+#ifdef DSR_EXP_SURFLS2        // A/B: surface tiles of the exact pass on the exact pass's chain
+constexpr int SURF_LS = 2;
+#else
+constexpr int SURF_LS = JFWD_LS;
+#endif
+#if defined(DSR_EXP_FLS0)
+constexpr int FWD_LS = 0;
+#elif defined(DSR_EXP_FLS2)
+constexpr int FWD_LS = 2;
+#else
+constexpr int FWD_LS = 1;
+#endif
 
 // power-of-two scale exponent s such that m * 2^s < 2^14 (m >= 0); 0 for m == 0 / non-finite
 __device__ __forceinline__ int act_scale_exp(float m) {
@@ -840,7 +926,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     for (int l = 1; l <= 6; ++l) {
       const int lane = opaque(threadIdx.x & 63);
       stamp(7);
-      gemm16_sel<PRIO, NB>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
+      if (SURF_LS != FWD_LS && surf) gemm16_sel<PRIO, NB, SURF_LS>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
+      else gemm16_sel<PRIO, NB, FWD_LS>(D.Wh_raw[l], w, D.Kf[l] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
       uint64_t mk;
       sa = epi16(acc, D.sw[l] + sa.b, (l == 4) ? bias4f + tl.obj * HID : D.bias[l], sm, w, lane, mk,
@@ -853,7 +940,8 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
     {
       const int lane = opaque(threadIdx.x & 63);
       stamp(7);
-      gemm16_sel<PRIO, NB>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
+      if (SURF_LS != FWD_LS && surf) gemm16_sel<PRIO, NB, SURF_LS>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
+      else gemm16_sel<PRIO, NB, FWD_LS>(D.Wh_raw[7], w, D.Kf[7] / 32, sm.Hh, sm.Hl, acc, lane, sa.resc());
       stamp(1);
       const int un = D.sw[7] + sa.b;
 #pragma unroll

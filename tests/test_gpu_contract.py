@@ -252,8 +252,10 @@ def test_ens256_distribution_per_iteration(gpu_decoder, name):
     the reference cloud's sigma, K in render points — at most 1.5x the largest the oracle shows
     over the trajectory, plus 3 standard errors; the KS distances are printed.  At the end the
     clouds must agree as distributions: final rotation / translation / code / loss deviations
-    from the reference's unperturbed result KS p >= 1e-3, medians within 2x, final-loss means
-    within 3 SE."""
+    from the reference's unperturbed result KS p >= 1e-3, medians within 2x, final-loss mean
+    offset at most 1.5x the oracle's + 3 SE (the oracle itself sits 4.2 SE from the reference on
+    kitti0).  kitti5 (round 5): largest per-iteration offset 0.70 of its bound (iteration 1;
+    round 4's kernels: 1.08), final KS p 0.25-0.55 (round 4: 5e-5 on the loss)."""
     from scipy.stats import ks_2samp
 
     from reconstruct.optimizer import Optimizer
@@ -306,8 +308,15 @@ def test_ens256_distribution_per_iteration(gpu_decoder, name):
               f"(ratio {med:.2f}) KS p {p:.3f}")
         assert p >= 1e-3 and 0.5 <= med <= 2.0, (c, p, med)
         worst = min(worst, p)
+    # final-loss means: the fp32 oracle's own offset from the reference is 4.2 standard errors on
+    # kitti0 (1.3 on kitti5), so "within 3 SE" would fail a correct fp32 implementation; held as
+    # the per-iteration offsets above: at most 1.5x the oracle's offset + 3 SE
     se = np.sqrt((g_loss.var(ddof=1) + r_loss.var(ddof=1)) / n)
-    assert abs(g_loss.mean() - r_loss.mean()) <= 3 * se
+    o_loss = o256["loss"].astype(np.float64)
+    off_o = abs(o_loss.mean() - r_loss.mean())
+    print(f"final-loss mean offset from the reference: gpu {(g_loss.mean() - r_loss.mean()) / se:+.2f} SE, "
+          f"oracle {(o_loss.mean() - r_loss.mean()) / se:+.2f} SE")
+    assert abs(g_loss.mean() - r_loss.mean()) <= 1.5 * off_o + 3 * se
     print(f"smallest KS p over the 4 final marginals: {worst:.3f}")
 
 
@@ -329,28 +338,34 @@ def test_ens_per_iteration_vs_exact_arithmetic(gpu_decoder, name):
     with the reference's fp32 chain gives the same 1.11), not torch's thread count (the
     reference's 8-thread cloud, golden F18, sits within 0.23 sigma of its 1-thread one).
 
-    Held at every iteration:
-    * accuracy — the GPU's RMS deviation from exact arithmetic at most 4x the larger of the two
-      fp32 implementations' (the reference F13, the fp32 oracle F16, same 64 starts): 4x is the
-      per-product rounding of the 3xFP16 split's 22-bit operands against fp32's 24 bits
-      (DESIGN.md §3.7), the dtype the bench line reports;
-    * no drift — the GPU's mean deviation from exact arithmetic within 3 standard errors (of the
-      64 paired deviations) plus 4x the larger |mean deviation| of the two fp32 implementations
-      (in the first iterations the members share one state, so an implementation's rounding there
-      is one number, common to all members — a mean, not noise: kitti0 iteration 3 has the
-      reference and the fp32 oracle both +4.5e-4 from exact, the GPU +8.0e-4, which the same
-      bound without the 4x missed by 2%).
+    Held at every iteration, against the larger of the two fp32 implementations' figures (the
+    reference F13 and the fp32 oracle F16, same 64 starts), all at 1.5x:
+    * loss — RMS deviation from exact at most 1.5x theirs; mean deviation within 3 standard
+      errors (of the 64 paired deviations) plus 1.5x their larger |mean deviation| (in the first
+      iterations the members share one state, so an implementation's rounding there is one
+      number common to all members — a mean, not noise);
+    * K — an integer count whose deviations are a bulk plus rare jumps: on kitti5 at iteration 2
+      most members sit within 9 render points of exact, and a few jump by 41-47 (one set of
+      band samples switching together) — the reference has 1 such member of 64, the fp32
+      oracle 0, split-kernel variants measured in round 5 0-3, so the RMS there counts jumps, a
+      binomial event at p ~ 2%, and 1.5x of it cannot be held by any implementation.  So: the
+      90th percentile of |deviation| (the bulk) at most 1.5x theirs + 1 render point, the
+      number of members beyond max(3, 3x their 90th percentile) not significantly larger than
+      theirs (one-sided Fisher exact test, p >= 1e-3), and the mean as for the loss.  Round 4's
+      kernels fail this on kitti5 (bulk 6.9x theirs: the Jacobian's rounding bias, below);
     * final states — rotation / translation / code / loss deviations from each member's exact
-      final state, RMS, at most 4x the fp32 implementations'.
-    Measured (r4 box, offline from tools/gpu_ens_dump.py): loss RMS at most 1.00x (kitti0) /
-    1.40x (kitti5) the fp32 implementations'; K RMS 1.05x / 2.56x (kitti5 iteration 2: 16.6 of
-    3,589 render points against 6.5); mean deviations at most 0.37 / 0.62 of their bound; final
-    states 0.79-0.98x / 0.79-1.35x.  On kitti5, whose clouds spread 5x wider than kitti0's (loss
-    sigma 5.7% at iteration 9), the GPU's final-loss cloud is ~30% wider than the reference's
-    (median deviation 5.4e-2 vs 4.2e-2, KS p 5e-5 at n = 256): the 1.35x RMS from exact
-    arithmetic above, carried through ten chaotic steps; the KS statistics are printed, not held,
-    on this object."""
-    from scipy.stats import ks_2samp
+      final state, RMS, at most 1.5x the fp32 implementations'.
+    Round 4 needed 4x here: the split's Jacobian carried a fixed bias of ~5e-8 of |J| (its
+    weights' rounded-away tails, and the f16 MFMA's rounding of the lo products onto the running
+    sum), which b = sum_p J_p r_p — cancelling to ~1e-5 of its terms on a converging object —
+    turned into pose-row errors 3-4x an fp32 Jacobian's (tools/member_step_dump.py against the
+    fp64 oracle's step).  Round 5: second-moment feedback rounding of the packs and lo products
+    chained from zero.
+    Measured (r5 box, offline from tools/gpu_ens_dump.py, the same batch; of each bound): loss RMS
+    0.73 (kitti0) / 0.89 (kitti5), loss mean 0.93 / 0.66, K bulk 0.73 / 0.84, K tails p >= 0.12,
+    K mean 0.62 / 0.34, final states 0.89-1.05x / 0.90-1.16x the fp32 implementations'.  The final
+    clouds against the reference's own (all 256 members) are printed: KS p >= 0.25 on both."""
+    from scipy.stats import fisher_exact, ks_2samp
 
     from reconstruct.optimizer import Optimizer
 
@@ -373,19 +388,31 @@ def test_ens_per_iteration_vs_exact_arithmetic(gpu_decoder, name):
     kx, kr, ko = (g["it_k"][:m].astype(np.float64) for g in (x64, e256, o256))
     kg = np.array([t["k"] for t in tr], np.float64)[:m]
     n_it = int(f["n_iters_run"])
+    rms = lambda d: float(np.sqrt(np.mean(d * d)))  # noqa: E731
+    q90 = lambda d: float(np.quantile(np.abs(d), 0.9))  # noqa: E731
     for e in range(n_it):
         scale = lx[:, e].mean()
-        for what, xs, xg, xx, unit in (("loss", (lr, lo), lg, lx, scale), ("K", (kr, ko), kg, kx, 1.0)):
-            dev = lambda a: (a[:, e] - xx[:, e]) / unit  # noqa: E731
-            rms = lambda d: float(np.sqrt(np.mean(d * d)))  # noqa: E731
-            d_g, d_f = dev(xg), [dev(a) for a in xs]
-            rms_f = max(rms(d) for d in d_f)
-            bias_f = max(abs(float(d.mean())) for d in d_f)
-            se_g = float(d_g.std(ddof=1)) / np.sqrt(m)
-            print(f"{name} it {e} {what}: rms vs exact gpu {rms(d_g):.2e} ref {rms(d_f[0]):.2e} oracle32 "
-                  f"{rms(d_f[1]):.2e} | mean gpu {d_g.mean():+.2e} ref {d_f[0].mean():+.2e} oracle32 {d_f[1].mean():+.2e}")
-            assert rms(d_g) <= 4.0 * rms_f + 1e-12, (what, e, rms(d_g), rms_f)
-            assert abs(float(d_g.mean())) <= 3 * se_g + 4.0 * bias_f + 1e-12, (what, e, float(d_g.mean()), se_g, bias_f)
+        d_g, d_f = (lg[:, e] - lx[:, e]) / scale, [(a[:, e] - lx[:, e]) / scale for a in (lr, lo)]
+        rms_f, bias_f = max(rms(d) for d in d_f), max(abs(float(d.mean())) for d in d_f)
+        se_g = float(d_g.std(ddof=1)) / np.sqrt(m)
+        print(f"{name} it {e} loss: rms vs exact gpu {rms(d_g):.2e} ref {rms(d_f[0]):.2e} oracle32 {rms(d_f[1]):.2e}"
+              f" | mean gpu {d_g.mean():+.2e} ref {d_f[0].mean():+.2e} oracle32 {d_f[1].mean():+.2e}")
+        assert rms(d_g) <= 1.5 * rms_f + 1e-12, ("loss", e, rms(d_g), rms_f)
+        assert abs(float(d_g.mean())) <= 3 * se_g + 1.5 * bias_f + 1e-12, ("loss", e, float(d_g.mean()), se_g, bias_f)
+        k_g, k_f = kg[:, e] - kx[:, e], [a[:, e] - kx[:, e] for a in (kr, ko)]
+        q_f = max(q90(d) for d in k_f)
+        thr = max(3.0, 3.0 * q_f)
+        tail = lambda d: int((np.abs(d) > thr).sum())  # noqa: E731
+        p_tail = min(fisher_exact([[tail(k_g), m - tail(k_g)], [tail(d), m - tail(d)]], alternative="greater")[1]
+                     for d in k_f)
+        kb_f = max(abs(float(d.mean())) for d in k_f)
+        se_k = float(k_g.std(ddof=1)) / np.sqrt(m)
+        print(f"{name} it {e} K: |dev| q90 gpu {q90(k_g):.1f} ref {q90(k_f[0]):.1f} oracle32 {q90(k_f[1]):.1f}; beyond "
+              f"{thr:.0f}: gpu {tail(k_g)} ref {tail(k_f[0])} oracle32 {tail(k_f[1])} (p {p_tail:.3f}); rms gpu "
+              f"{rms(k_g):.1f} ref {rms(k_f[0]):.1f} oracle32 {rms(k_f[1]):.1f}; mean gpu {k_g.mean():+.2f}")
+        assert q90(k_g) <= 1.5 * q_f + 1.0, ("K bulk", e, q90(k_g), q_f)
+        assert p_tail >= 1e-3, ("K tails", e, tail(k_g), [tail(d) for d in k_f])
+        assert abs(float(k_g.mean())) <= 3 * se_k + 1.5 * kb_f + 1e-12, ("K mean", e, float(k_g.mean()), se_k, kb_f)
     # final states: each member's rotation / translation / code / loss deviation from its exact
     # final state (F19), RMS over the 64 members, against the fp32 implementations'
     def dev(T, z, loss, k):
@@ -396,12 +423,12 @@ def test_ens_per_iteration_vs_exact_arithmetic(gpu_decoder, name):
                 np.abs(np.asarray(z, np.float64) - zx).max() / np.abs(zx).max(),
                 abs(float(loss) - float(x64["loss"][k])) / abs(float(x64["loss"][k])))
 
-    rms = lambda a: np.sqrt((np.asarray(a) ** 2).mean(0))  # noqa: E731
+    rms = lambda a: np.sqrt((np.asarray(a) ** 2).mean(0))  # noqa: E731, F811
     fin_g = rms([dev(res[k]["t_cam_obj"], res[k]["code"], res[k]["loss"], k) for k in range(m)])
     fin_f = np.maximum(*[rms([dev(g["t_cam_obj"][k], g["code"][k], g["loss"][k], k) for k in range(m)]) for g in (e256, o256)])
     print(f"{name} final vs exact (rot, t, code, loss) RMS gpu {np.array2string(fin_g, precision=2)} fp32 "
           f"{np.array2string(fin_f, precision=2)}")
-    assert (fin_g <= 4.0 * fin_f).all(), (fin_g, fin_f)
+    assert (fin_g <= 1.5 * fin_f).all(), (fin_g, fin_f)
     # and, for the record, the final clouds against the reference's own (all 256 members)
     g_err = np.array([contract_errors(r["t_cam_obj"], r["code"], r["loss"], f) for r in res])
     r_err = np.array([contract_errors(e256["t_cam_obj"][k], e256["code"][k], e256["loss"][k], f) for k in range(n)])

@@ -59,7 +59,16 @@ def test_variant_decoder_vs_golden(decs, v):
 @pytest.mark.parametrize("v", ["tanh", "xyz", "ln"])
 def test_variant_teacher_forced_steps(decs, v):
     """Every recorded reference state -> one GPU GN step: K, loss, H, b and the step at the
-    shipped topology's teacher-forced tolerances (tests/test_gpu_parity.py)."""
+    shipped topology's teacher-forced tolerances (tests/test_gpu_parity.py).  Where the GPU's
+    render set differs from the reference's (dK != 0: band samples on the |sdf| = th or
+    de_do = 1e-2 thresholds, which any two fp32 implementations can decide either way) the step
+    moves by that render point's own share of H and b, whatever its size: the fp32 oracle
+    re-takes the step from the same state, and if it made the GPU's decision (same K) the GPU's
+    step is held to it at the identical-render-set tolerances; otherwise to the reference's at
+    the flipped-point ones.  (Round 5, LayerNorm iteration 1: dK 1 against the reference, b off
+    by 6.7e-3 of its max, against the oracle with the same K dK 0.)"""
+    from oracle import dsr_oracle as O
+
     f = golden("f17_variants.npz")
     one = dict(KITTI3, joint_optim=dict(KITTI3["joint_optim"], num_iterations=1))
     opt = _opt(decs[v], one)
@@ -68,6 +77,7 @@ def test_variant_teacher_forced_steps(decs, v):
              f[v + "_it_z"][e]) for e in range(n_it)]
     res, tr = opt.reconstruct_objects(objs, trace=True, pose_is_obj_cam=True)
     jo = KITTI3["joint_optim"]
+    odec = None
     for e in range(n_it):
         t = tr[e]
         assert res[e]["is_good"]
@@ -75,15 +85,25 @@ def test_variant_teacher_forced_steps(decs, v):
         assert dk <= 2
         loss_ref = jo["k1"] * f[v + "_it_render_loss"][e] + jo["k2"] * f[v + "_it_sdf_loss"][e]
         assert abs(t["loss"][0] - loss_ref) <= 1e-5 * abs(loss_ref) + dk * jo["k1"] * 0.09 / f[v + "_it_k"][e]
+        H_r, b_r, dx_r = (np.asarray(f[v + "_it_" + k][e], np.float64) for k in ("H", "b", "dx"))
+        who = "ref"
+        if dk != 0:
+            if odec is None:
+                odec = O.Decoder.from_state(S.make_decoder(1234, _variant_specs(v)), _variant_specs(v))
+            n_fg = f[v + "_obj_depth"].shape[0]
+            dobs = np.concatenate([f[v + "_obj_depth"], np.zeros(f[v + "_obj_rays"].shape[0] - n_fg)]).astype(np.float32)
+            tro, _, _ = O.gn_step(odec, O.OptimParams.from_cfg(KITTI3), np.asarray(f[v + "_it_t_obj_cam"][e]),
+                                  np.asarray(f[v + "_it_z"][e]), f[v + "_obj_pts"], f[v + "_obj_rays"], dobs, n_fg)
+            if int(tro.k) == int(t["k"][0]):
+                H_r, b_r, dx_r = (np.asarray(a, np.float64) for a in (tro.H, tro.b, tro.dx))
+                dk, who = 0, "oracle32"
         H, b, dx = (np.asarray(t[k][0], np.float64) for k in ("H", "b", "dx"))
-        eh = rel(H, f[v + "_it_H"][e])
+        eh = rel(H, H_r)
         rest = np.r_[0:3, 6:71]
-        eb = rel(b[rest], f[v + "_it_b"][e][rest])
-        d = dx - f[v + "_it_dx"][e]
-        Hr = np.asarray(f[v + "_it_H"][e], np.float64)
-        dr = np.asarray(f[v + "_it_dx"][e], np.float64)
-        es = float(np.sqrt(max(d @ Hr @ d, 0.0) / max(dr @ Hr @ dr, 1e-300)))
-        print(f"{v} it {e}: dK {dk} H {eh:.2e} b {eb:.2e} dx(H-norm) {es:.2e}")
+        eb = rel(b[rest], b_r[rest])
+        d = dx - dx_r
+        es = float(np.sqrt(max(d @ H_r @ d, 0.0) / max(dx_r @ H_r @ dx_r, 1e-300)))
+        print(f"{v} it {e}: vs {who} dK {dk} H {eh:.2e} b {eb:.2e} dx(H-norm) {es:.2e}")
         assert eh <= (5e-4 if dk == 0 else 2e-3)
         assert eb <= (5e-4 if dk == 0 else 5e-3)
         assert es <= 1e-2
