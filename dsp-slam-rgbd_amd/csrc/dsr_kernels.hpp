@@ -1198,15 +1198,17 @@ struct Jac16Shared {
   float wmax[NWAVE];
 };
 
-// The backward GEMMs (W_l^T) chain their lo products from zero (gemm16_sel's LS, dsr_mlp16.hpp),
-// as the forward ones do: the Jacobian's own rounding bias then no longer dominates its error
+// The backward GEMMs (W_l^T) keep their lo products off the running sum (gemm16_sel's LS 2,
+// dsr_mlp16.hpp), as the forward ones do: the Jacobian's own rounding bias then no longer dominates its error
 // (tools/bias_probe.py: J bias 3.4e-8 -> 2.3e-8 of |J|, random 8.3e-7 -> 5.8e-7; fp32 numpy
 // 5.7e-9 / 7.2e-7) — the sum b = sum_p J_p r_p cancels to ~1e-5 of its terms on a converging
 // object, so that bias, not the random error, is what its pose rows see.
-#ifdef DSR_EXP_NOLS
+#if defined(DSR_EXP_NOLS)
 constexpr int BWD_LS = 0;
-#else
+#elif defined(DSR_EXP_BLS1)
 constexpr int BWD_LS = 1;
+#else
+constexpr int BWD_LS = 2;
 #endif
 
 // NB: A ring depth of the split GEMMs (gemm16_sel; 0 = the two-set gemm16_tile).  Lane-derived
@@ -1568,7 +1570,7 @@ __global__ __launch_bounds__(512) void k_mlp_jac16(DevDecoder D, const Tile* __r
     if (w < 5) {
       const int lane = opaque(threadIdx.x & 63), g = lane >> 4, c = lane & 15;
       floatx4 a1[1][4];
-      gemm16_tile<PRIO, 1, 0, BWD_LS>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
+      gemm16_tile<PRIO, 1, 0, (BWD_LS != 0)>(reinterpret_cast<const half8*>(D.Wbh_raw[0]) + (size_t)w * 16 * 2 * 64, 16,
                            sm.Hh, sm.Hl, a1, lane);
       const int un = D.swb[0] + sa;
 #pragma unroll

@@ -87,13 +87,16 @@ __device__ __forceinline__ int h_boff(int lane) {
   return c * PH + 8 * ((lane >> 4) ^ ((c >> 2) & 1));
 }
 
-// LS (every split GEMM): each k step's two lo products chained from zero and added to the
-// running sum on the VALU (round to nearest) instead of onto it in the MFMA.
-// The f16 MFMA rounds each 8-deep chunk sum onto its accumulator toward -inf to about an ulp of
-// the ACCUMULATOR (tools/mfma_numerics.py): chained onto the large running sum, the two small lo
-// products cost two such roundings per k step for ~2^-11 of the product's value; from zero they
-// round to their own size.  Measured on one decoder-layer-shaped block (tools/split_chain_bias.py):
-// mean error -1.36e-8 -> -1.6e-9 of |exact|, rms 2.4e-7 -> 1.6e-7.
+// LS: the two lo products of a split GEMM kept off the running sum.  The f16 MFMA rounds each
+// 8-deep chunk sum onto its accumulator toward -inf to about an ulp of the ACCUMULATOR
+// (tools/mfma_numerics.py): chained onto the large running sum, the two small lo products cost two
+// such roundings per k step for ~2^-11 of the product's value.  Measured on one decoder-layer-
+// shaped block (tools/split_chain_bias.py): mean error -1.36e-8 of |exact| on the plain chain,
+// -1.6e-9 with the lo products from zero, rms 2.4e-7 -> 1.6e-7.  LS 2 (every shipped split GEMM,
+// gemm16_ring): the lo products in their own accumulators over the whole k loop, one VALU add per
+// output at the end (64 more VGPRs; the kernels fit them: 0 / 36 / 72 B of scratch).  LS 1 (this
+// tile path: lin0^T, the NB = 0 A/B kernels): each k step's lo pair chained from zero and added on
+// the VALU — 64 adds per k step beside 48 MFMAs, +14% per split launch when every GEMM ran it.
 template <bool PRIO, int NQ, int EX = 0, bool LS = false>
 __device__ __forceinline__ void mfma3_step(const half8 (&ah)[NQ], const half8 (&al)[NQ], const half8 (&bh)[4],
                                            const half8 (&bl)[4], floatx4 (&acc)[NQ][4]) {
@@ -396,28 +399,27 @@ __device__ __forceinline__ void gemm16_sel(const _Float16* Wl, int w, int T, con
   }
 }
 
-// Every split GEMM chains its lo products per k step from zero (LS 1).  The exact pass could
-// keep them in their own accumulators over the whole k loop instead (LS 2: 64 more VGPRs, which
-// k_mlp_fwd16 has to spare, one VALU add per output; DSR_EXP_FLS2) and the bench gained ~2%, but
-// the Jacobian kernel has no VGPRs to spare for it, and a sample's masks and sdf must be the same
-// bits whichever kernel computes them (test_gpu_parity.py: the lite pass against the exact
-// decode, the broken-block fallback; test_gpu_bench.py: 8-rank shards against one rank).
-#ifdef DSR_EXP_JFLS0
+// Every forward and backward split GEMM keeps its lo products in their own accumulators (LS 2).
+// The chain must be the same in every kernel that forwards a point: a sample's masks and sdf are
+// the same bits whichever kernel computes them (test_gpu_parity.py: the lite pass against the
+// exact decode, the broken-block fallback, the surface forward of small batches;
+// test_gpu_bench.py: 8-rank shards against one rank).
+#if defined(DSR_EXP_JFLS0)
 constexpr int JFWD_LS = 0;
-#else
+#elif defined(DSR_EXP_JFLS1)
 constexpr int JFWD_LS = 1;
-#endif
-#ifdef DSR_EXP_SURFLS2        // A/B: surface tiles of the exact pass on the exact pass's chain
-constexpr int SURF_LS = 2;
 #else
-constexpr int SURF_LS = JFWD_LS;
+constexpr int JFWD_LS = 2;
 #endif
+// the exact pass's surface tiles run the Jacobian kernel's forward chain (the same one unless an
+// A/B build sets them apart)
+constexpr int SURF_LS = JFWD_LS;
 #if defined(DSR_EXP_FLS0)
 constexpr int FWD_LS = 0;
-#elif defined(DSR_EXP_FLS2)
-constexpr int FWD_LS = 2;
-#else
+#elif defined(DSR_EXP_FLS1)
 constexpr int FWD_LS = 1;
+#else
+constexpr int FWD_LS = 2;
 #endif
 
 // power-of-two scale exponent s such that m * 2^s < 2^14 (m >= 0); 0 for m == 0 / non-finite

@@ -404,3 +404,28 @@ def test_oracle_decoder_variants(v):
         assert abs(tr.loss - loss_ref) <= 1e-5 * abs(loss_ref) + dk * jo["k1"] * 0.09 / f[v + "_it_k"][e]
         assert rel(tr.H, f[v + "_it_H"][e]) <= (3e-3 if dk == 0 else 1e-2)
         assert rel(tr.b, f[v + "_it_b"][e]) <= (1e-2 if dk == 0 else 3e-2)
+
+
+def test_f8_conditioning_record_reproduces():
+    """tests/golden/f8_conditioning.json (tools/f8_conditioning.py), which the strict GPU contract
+    test reads to tell a well-conditioned margin fixture from one whose GN step amplifies an
+    fp32-sized state error out of the contract: the ill-conditioned entry (redwood_s5359,
+    iteration 2: the fp32 oracle's own 2e-6 state error -> 1.9e-2 in the next state) and one
+    well-conditioned entry recomputed here with the fp64 oracle, same seed."""
+    import json
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import f8_conditioning as FC
+
+    rec = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "f8_conditioning.json")))
+    d64, d32 = FC.decoders()
+    for name in ("redwood_s5359", "redwood3it_s5006"):
+        c = FC.conditioning(os.path.join(os.path.dirname(__file__), "golden", f"f8_margin_{name}.npz"), d64, d32)
+        r = rec["fixtures"][name]
+        assert c["well_conditioned"] == r["well_conditioned"], name
+        np.testing.assert_allclose(c["worst_next_state_deviation"], r["worst_next_state_deviation"], rtol=1e-6)
+    assert not rec["fixtures"]["redwood_s5359"]["well_conditioned"]
+    assert rec["fixtures"]["redwood_s5359"]["worst_next_state_deviation"][2] > 1e-2
+    assert sum(e["well_conditioned"] for e in rec["fixtures"].values()) >= 9
