@@ -412,10 +412,10 @@ def test_ens_per_iteration_vs_exact_arithmetic(gpu_decoder, name):
     turned into pose-row errors 3-4x an fp32 Jacobian's (tools/member_step_dump.py against the
     fp64 oracle's step).  Round 5: second-moment feedback rounding of the packs and lo products
     chained from zero.
-    Measured (r5 box, offline from tools/gpu_ens_dump.py, the same batch; of each bound): loss RMS
-    0.73 (kitti0) / 0.89 (kitti5), loss mean 0.93 / 0.66, K bulk 0.73 / 0.84, K tails p >= 0.12,
-    K mean 0.62 / 0.34, final states 0.89-1.05x / 0.90-1.16x the fp32 implementations'.  The final
-    clouds against the reference's own (all 256 members) are printed: KS p >= 0.25 on both."""
+    Measured (r5 box, offline from tools/gpu_ens_dump.py on the same batch, tools/ens_judge.py;
+    of each bound): loss RMS 0.79 (kitti0) / 0.86 (kitti5), loss mean 0.89 / 0.64, K bulk
+    0.72 / 0.92, K tails p >= 0.1, K mean 0.57 / 0.43, final states 0.71 / 0.77.  The final
+    clouds against the reference's own (all 256 members) are printed: KS p >= 0.04 on both."""
     from scipy.stats import fisher_exact, ks_2samp
 
     from reconstruct.optimizer import Optimizer
