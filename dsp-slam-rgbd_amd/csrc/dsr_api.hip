@@ -292,6 +292,7 @@ struct dsr_batch {
   bool ran = false;
   int runs = 0;
   bool timed = false;               // last run recorded per-kernel events (eager run)
+  bool prescan = false;             // first pass's ray scan over the ray chunks (k_sample_scan)
   hipGraphExec_t graph = nullptr;   // the whole run, captured on the 2nd dsr_batch_run
   long graph_key = -1;              // kernel variants the graph was captured with
   int captures = 0, replays = 0;    // graph captures / replays over the batch's life
@@ -302,6 +303,7 @@ struct dsr_batch {
   bool capacity = false;
   bool cap_graph = false;           // DSR_BATCH_GRAPH: every run replays one captured graph
   int max_pts = 0, max_rays = 0;
+  size_t pts_floats = 0, ray_slots = 0;   // pts / rays+dobs buffer lengths (group padding included)
   int n_active = 0;                 // objects of the current fill (out-records downloaded)
   struct Stage {                    // pinned host mirrors of the refilled input buffers
     void* host = nullptr;
@@ -1064,9 +1066,63 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   const int M = b->M;
   std::vector<float> hpts, hrays, hdobs, hz((size_t)n_obj * CODE, 0.f), ht((size_t)n_obj * 16);
   std::vector<int> hoc(n_obj), ftile_o(n_obj), jtile_o(n_obj);
+  long cand_est = 0;                         // ray samples of the batch (group count heuristic)
+  for (int o = 0; o < n_obj; ++o) cand_est += (long)std::max(0, in[o].n_rays) * M;
+  {
+    // object groups on concurrent streams (DESIGN.md §3.5): 2 for large batches (the decoder
+    // grids fill the chip; more groups only overlap their launches), 4 for small batches of
+    // large objects (a strong-scaled shard of 8-16 KITTI objects is bound by its latency
+    // kernels, which the extra groups hide: 8 objects 317 -> 333 obj/s), 2 again for small
+    // batches of small objects (8 Redwood keyframe hypotheses: 5.31 -> 5.16 ms)
+    // Under DSR_GRAPH=1 the default is ONE group: ROCm 7.2 replays a captured multi-stream
+    // fork/join as a graph 1.6x slower than the eager groups (keyframe batch 8.4 vs 5.2 ms,
+    // whatever DEBUG_HIP_FORCE_GRAPH_QUEUES / DEBUG_CLR_GRAPH_PACKET_CAPTURE say), while a
+    // one-group graph replays 3% faster than a one-group eager run (5.31 vs 5.46 ms; r3k,
+    // tools/graph_queues.py).  Results are bitwise the same for any grouping.
+    const char* e = getenv("DSR_STREAMS");
+    int G = e ? atoi(e) : (graph_enabled() || one_group) ? 1 : ((n_obj <= 16 && cand_est >= 500000) ? 4 : 2);
+    G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
+    if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
+    for (int g = 0; g < G; ++g) {
+      dsr_batch::Group gr;
+      gr.o0 = (int)((long)n_obj * g / G);
+      gr.n = (int)((long)n_obj * (g + 1) / G) - gr.o0;
+      b->groups.push_back(gr);
+    }
+    if (dec->D.ln_mask)
+      for (int g = 0; g < G; ++g)
+        if (!ln_workspace(ctx, g)) {
+          dsr_batch_destroy(b);
+          return fail(ctx, "hipMalloc failed (LayerNorm workspace)");
+        }
+  }
+  // Every group's slices of the per-ray / per-sample / per-point / per-slot buffers start on
+  // a fresh 256 B line (zero padding between groups): the groups' kernels run concurrently on
+  // their own streams, and a cache line holding both groups' elements (the dead flags of the
+  // last rays of one group and the first of the next) was written by both at once — the
+  // run-to-run variable decode counts of DESIGN.md §3.9.  DSR_GROUP_ALIGN=0 (test hook) packs
+  // the groups back to back for that comparison.
+  bool galign = true;
+  {
+    const char* e = hook_env("DSR_GROUP_ALIGN");
+    if (e && atoi(e) == 0) galign = false;
+  }
+  std::vector<char> gfirst(n_obj, 0);
+  auto up_to = [](int v, int a) { return (int)std::min<long>(INT_MAX, ((long)v + a - 1) / a * a); };
+  for (size_t g = 1; g < b->groups.size(); ++g) gfirst[b->groups[g].o0] = 1;
   int pts_off = 0, ray_off = 0, cand_off = 0, slot_off = 0, ftiles = 0;
   for (int o = 0; o < n_obj; ++o) {
     const dsr_object_in& x = in[o];
+    if (galign && gfirst[o]) {
+      const int r1 = up_to(ray_off, 64), c1 = up_to(cand_off, 256), p1 = up_to(pts_off, 64);
+      hrays.resize((size_t)r1 * 3, 0.f);
+      hdobs.resize((size_t)r1, 0.f);
+      hpts.resize((size_t)p1 * 3, 0.f);
+      ray_off = r1;
+      cand_off = c1;
+      pts_off = p1;
+      slot_off = up_to(slot_off, 8);
+    }
     // Empty inputs are the reference's numeric failures, not errors: no surface points make
     // the sdf loss a mean of nothing (NaN, optimizer.py:137), no rays leave < 10 in-ball
     // samples (loss.py:86-88) — is_good = False, loss 0., exactly as there (golden F10)
@@ -1103,34 +1159,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ftiles += ftile_o[o];
     slot_off += jtile_o[o];
   }
-  {
-    // object groups on concurrent streams (DESIGN.md §3.5): 2 for large batches (the decoder
-    // grids fill the chip; more groups only overlap their launches), 4 for small batches of
-    // large objects (a strong-scaled shard of 8-16 KITTI objects is bound by its latency
-    // kernels, which the extra groups hide: 8 objects 317 -> 333 obj/s), 2 again for small
-    // batches of small objects (8 Redwood keyframe hypotheses: 5.31 -> 5.16 ms)
-    // Under DSR_GRAPH=1 the default is ONE group: ROCm 7.2 replays a captured multi-stream
-    // fork/join as a graph 1.6x slower than the eager groups (keyframe batch 8.4 vs 5.2 ms,
-    // whatever DEBUG_HIP_FORCE_GRAPH_QUEUES / DEBUG_CLR_GRAPH_PACKET_CAPTURE say), while a
-    // one-group graph replays 3% faster than a one-group eager run (5.31 vs 5.46 ms; r3k,
-    // tools/graph_queues.py).  Results are bitwise the same for any grouping.
-    const char* e = getenv("DSR_STREAMS");
-    int G = e ? atoi(e) : (graph_enabled() || one_group) ? 1 : ((n_obj <= 16 && (long)cand_off >= 500000) ? 4 : 2);
-    G = std::max(1, std::min(std::min(G, MAX_GROUPS), n_obj));
-    if (fwd_variant() & 1) G = 1;             // the XCD soft sync assumes one fwd grid at a time
-    for (int g = 0; g < G; ++g) {
-      dsr_batch::Group gr;
-      gr.o0 = (int)((long)n_obj * g / G);
-      gr.n = (int)((long)n_obj * (g + 1) / G) - gr.o0;
-      b->groups.push_back(gr);
-    }
-    if (dec->D.ln_mask)
-      for (int g = 0; g < G; ++g)
-        if (!ln_workspace(ctx, g)) {
-          dsr_batch_destroy(b);
-          return fail(ctx, "hipMalloc failed (LayerNorm workspace)");
-        }
-  }
+  // (the surface points' mask / sdf slots follow the samples': their groups' slices too)
+  if (galign && b->groups.size() > 1) cand_off = up_to(cand_off, 256);
   b->cand_total = cand_off;
   b->slot_total = slot_off;
   b->fwd_tile_cap = ftiles;
@@ -1144,6 +1174,8 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->z_in, sizeof(float) * CODE * n_obj);
   ALLOC(b->t_in, sizeof(float) * 16 * n_obj);
   ALLOC(b->is_oc, sizeof(int) * n_obj);
+  b->pts_floats = hpts.size();
+  b->ray_slots = hdobs.size();
   ALLOC(b->pts, sizeof(float) * hpts.size());
   ALLOC(b->rays, sizeof(float) * hrays.size());
   ALLOC(b->dobs, sizeof(float) * hdobs.size());
@@ -1152,6 +1184,10 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
+  {   // DSR_PRESCAN (test hook): the first pass's ray scan as its own chunked launch
+    const char* e = hook_env("DSR_PRESCAN");
+    b->prescan = e && atoi(e) != 0;
+  }
   {
     // the lite pass runs only on decoders that passed their load-time qualification
     // (decoder_qualify); DSR_LITE=0 decodes every sample exactly on any decoder
@@ -1217,17 +1253,17 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     }
   }
   ALLOC(b->slots, sizeof(float) * SLOT_FLOATS * (size_t)slot_off);
-  ALLOC(b->sred, sizeof(float) * 2 * SLOT_FLOATS * (size_t)n_obj);
+  ALLOC(b->sred, sizeof(float) * SRED_STRIDE * (size_t)n_obj);
   b->lite_cfg = lite_settings(b->hooks);
   b->loop_iters = b->iters + ((b->lite && b->lite_cfg.audit && b->iters > 0) ? 1 : 0);
   ALLOC(b->diag, sizeof(int) * STD_INTS);
-  ALLOC(b->counts, sizeof(int) * NCOUNT * (size_t)std::max(1, b->loop_iters) * n_obj);
+  ALLOC(b->counts, sizeof(int) * COUNT_STRIDE * (size_t)std::max(1, b->loop_iters) * n_obj);
   ALLOC(b->out, sizeof(dsr_object_out) * n_obj);
   if (trace) {
     const size_t it = std::max(1, b->iters);
-    ALLOC(b->tr_H, sizeof(float) * NPAR * NPAR * it * n_obj);
-    ALLOC(b->tr_v, sizeof(float) * TRACE_V * it * n_obj);
-    ALLOC(b->tr_i, sizeof(int) * 2 * it * n_obj);
+    ALLOC(b->tr_H, sizeof(float) * TRACE_H_STRIDE * it * n_obj);
+    ALLOC(b->tr_v, sizeof(float) * TRACE_V_STRIDE * it * n_obj);
+    ALLOC(b->tr_i, sizeof(int) * TRACE_I_STRIDE * it * n_obj);
   }
 #undef ALLOC
   auto up = [&](void* dst, const void* src, size_t bytes) {
@@ -1244,9 +1280,9 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     return fail(ctx, "hipMemcpy (inputs) failed");
   }
   if (trace) {
-    hipMemsetAsync(b->tr_H, 0, sizeof(float) * NPAR * NPAR * std::max(1, b->iters) * n_obj, ctx->stream);
-    hipMemsetAsync(b->tr_v, 0, sizeof(float) * TRACE_V * std::max(1, b->iters) * n_obj, ctx->stream);
-    hipMemsetAsync(b->tr_i, 0, sizeof(int) * 2 * std::max(1, b->iters) * n_obj, ctx->stream);
+    hipMemsetAsync(b->tr_H, 0, sizeof(float) * TRACE_H_STRIDE * std::max(1, b->iters) * n_obj, ctx->stream);
+    hipMemsetAsync(b->tr_v, 0, sizeof(float) * TRACE_V_STRIDE * std::max(1, b->iters) * n_obj, ctx->stream);
+    hipMemsetAsync(b->tr_i, 0, sizeof(int) * TRACE_I_STRIDE * std::max(1, b->iters) * n_obj, ctx->stream);
   }
   b->passes = render_passes(M, (long)cand_off, (long)ray_off, ctx->n_cu);
   b->ev.resize((size_t)std::max(1, b->loop_iters) * b->groups.size() * ev_per_iter(b) + 2);
@@ -1300,9 +1336,9 @@ int dsr_batch_create_capacity(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_op
   const std::pair<void*, size_t> bufs[] = {
       {b->desc, sizeof(ObjDesc) * max_obj},          {b->t_in, sizeof(float) * 16 * max_obj},
       {b->z_in, sizeof(float) * CODE * max_obj},     {b->is_oc, sizeof(int) * max_obj},
-      {b->pts, sizeof(float) * 3 * (size_t)max_obj * max_pts},
-      {b->rays, sizeof(float) * 3 * (size_t)max_obj * max_rays},
-      {b->dobs, sizeof(float) * (size_t)max_obj * max_rays}};
+      {b->pts, sizeof(float) * b->pts_floats},
+      {b->rays, sizeof(float) * 3 * b->ray_slots},
+      {b->dobs, sizeof(float) * b->ray_slots}};
   for (const auto& kv : bufs) {
     dsr_batch::Stage sg;
     sg.dev = kv.first;
@@ -1576,9 +1612,14 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       ert.diag = b->diag;
       DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
                                        (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
+      const bool pre = b->prescan && gr.n_rch > 0;
+      if (pre)                                   // the first pass's ray scan over the ray chunks
+        hipLaunchKernelGGL(k_sample_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                           b->M, b->dead, b->rinfo);
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo);
+                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo,
+                           (pz == 0 && pre) ? 1 : 0);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
                            b->lite ? LTILE : TILE, 0);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
@@ -1629,13 +1670,13 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
                          keep ? b->ma : MaskArgs{nullptr, nullptr, nullptr, nullptr},
                          D.ln_mask ? ctx->lnws[g] : (float*)nullptr);
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je + 1], s));
-      float* sred = b->sred + (size_t)o0 * 2 * SLOT_FLOATS;
+      float* sred = b->sred + (size_t)o0 * SRED_STRIDE;
       hipLaunchKernelGGL(k_reduce_slots, dim3(ng * SLOT_BLOCKS), dim3(256), 0, s, desc, st, b->slots, sred, it,
-                         b->counts + (size_t)o0 * NCOUNT, n);
+                         b->counts + (size_t)o0 * COUNT_STRIDE, n);
       hipLaunchKernelGGL(k_solve, dim3(ng), dim3(SOLVE_THREADS), 0, s, ng, desc, st, zbuf, P, sred,
-                         b->tr_H ? b->tr_H + (size_t)o0 * NPAR * NPAR : nullptr,
-                         b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V : nullptr,
-                         b->tr_i ? b->tr_i + (size_t)o0 * 2 : nullptr, n);
+                         b->tr_H ? b->tr_H + (size_t)o0 * TRACE_H_STRIDE : nullptr,
+                         b->tr_v ? b->tr_v + (size_t)o0 * TRACE_V_STRIDE : nullptr,
+                         b->tr_i ? b->tr_i + (size_t)o0 * TRACE_I_STRIDE : nullptr, n);
     }
   }
   for (int g = 1; g < G; ++g) {
@@ -1737,11 +1778,11 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
       st->lite_redo_objects += o.lite_redo ? 1 : 0;
     }
   }
-  std::vector<int> c((size_t)NCOUNT * std::max(1, b->loop_iters) * b->n_obj);
+  std::vector<int> c((size_t)COUNT_STRIDE * std::max(1, b->loop_iters) * b->n_obj);
   DSR_CHECK(b->ctx, hipMemcpy(c.data(), b->counts, sizeof(int) * c.size(), hipMemcpyDeviceToHost));
   for (int it = 0; it < used_iters; ++it)
     for (int o = 0; o < b->n_obj; ++o) {
-      const int* e = c.data() + ((size_t)it * b->n_obj + o) * NCOUNT;
+      const int* e = c.data() + ((size_t)it * b->n_obj + o) * COUNT_STRIDE;
       st->fwd_points += e[0];
       st->jac_points += e[1];
       st->inball_points += e[2];
@@ -1824,8 +1865,8 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
   if (!rc) rc = dsr_batch_download(b, out);
   if (!rc && trace) {
     const int it = b->iters;
-    std::vector<float> H((size_t)NPAR * NPAR * std::max(1, it) * n_obj), V((size_t)TRACE_V * std::max(1, it) * n_obj);
-    std::vector<int> I((size_t)2 * std::max(1, it) * n_obj);
+    std::vector<float> H((size_t)TRACE_H_STRIDE * std::max(1, it) * n_obj), V((size_t)TRACE_V_STRIDE * std::max(1, it) * n_obj);
+    std::vector<int> I((size_t)TRACE_I_STRIDE * std::max(1, it) * n_obj);
     if (hipMemcpy(H.data(), b->tr_H, sizeof(float) * H.size(), hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(V.data(), b->tr_v, sizeof(float) * V.size(), hipMemcpyDeviceToHost) != hipSuccess ||
         hipMemcpy(I.data(), b->tr_i, sizeof(int) * I.size(), hipMemcpyDeviceToHost) != hipSuccess) {
@@ -1835,8 +1876,8 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
         const dsr_trace& t = trace[o];
         for (int e = 0; e < it; ++e) {
           const size_t k = (size_t)e * n_obj + o;
-          if (t.H) std::memcpy(t.H + (size_t)e * NPAR * NPAR, H.data() + k * NPAR * NPAR, sizeof(float) * NPAR * NPAR);
-          const float* v = V.data() + k * TRACE_V;
+          if (t.H) std::memcpy(t.H + (size_t)e * NPAR * NPAR, H.data() + k * TRACE_H_STRIDE, sizeof(float) * NPAR * NPAR);
+          const float* v = V.data() + k * TRACE_V_STRIDE;
           if (t.b) std::memcpy(t.b + (size_t)e * NPAR, v, sizeof(float) * NPAR);
           if (t.dx) std::memcpy(t.dx + (size_t)e * NPAR, v + NPAR, sizeof(float) * NPAR);
           if (t.loss) t.loss[e] = v[2 * NPAR];
@@ -1844,8 +1885,8 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
           if (t.render_loss) t.render_loss[e] = v[2 * NPAR + 2];
           if (t.t_obj_cam) std::memcpy(t.t_obj_cam + (size_t)e * 16, v + 2 * NPAR + 3, sizeof(float) * 16);
           if (t.z) std::memcpy(t.z + (size_t)e * dec->code_len, v + 2 * NPAR + 19, sizeof(float) * dec->code_len);
-          if (t.n_valid) t.n_valid[e] = I[k * 2];
-          if (t.k) t.k[e] = I[k * 2 + 1];
+          if (t.n_valid) t.n_valid[e] = I[k * TRACE_I_STRIDE];
+          if (t.k) t.k[e] = I[k * TRACE_I_STRIDE + 1];
         }
       }
     }

@@ -127,7 +127,9 @@ struct ObjState {
   int lite_viol;         // this iteration's audited samples whose exact class differs
   int lite_viol_total;   // over the run
   int lite_redo;         // 1: an iteration was discarded for a violation; exact from then on
+  int pad_[8];           // whole 128 B lines per object: no line holds two groups' objects
 };
+static_assert(sizeof(ObjState) % 128 == 0, "ObjState spans whole cache lines");
 
 struct Tile {
   int obj, term, start, count;   // term: 0 = sdf (surface points), 1 = render (K list),
@@ -136,6 +138,22 @@ struct Tile {
 
 // Early ray termination (k_sample_pass): the fwd kernels flag a ray dead once one of its
 // samples decodes to sdf <= -cut_off (occupancy exactly 1, transmittance exactly 0 after it).
+// dead-flag accesses (experiment DSR_EXP_DEADWT: system-scope relaxed atomics, i.e. vector
+// loads / stores that bypass the non-coherent caches)
+__device__ __forceinline__ void dead_put(int* p, int v) {
+#ifdef DSR_EXP_DEADWT
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ int dead_get(int* p) {
+#ifdef DSR_EXP_DEADWT
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  return *p;
+#endif
+}
 struct ObjState;
 struct ErtArgs {
   int* dead;             // [sum n_rays] (nullptr: no flagging, e.g. dsr_sdf_eval)

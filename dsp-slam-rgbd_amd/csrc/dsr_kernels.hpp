@@ -342,11 +342,47 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// k_sample_scan: the first render pass's per-ray scan (each ray's in-ball run, loss.py:82; its
+// dead flag cleared) spread over the object group's 128-ray chunks, one thread per ray, instead
+// of one 1024-thread workgroup per object walking its rays in rounds; k_sample_pass then emits
+// the first window from the runs as later passes do.  Launched per object group with the
+// group's own descriptor / state slices and chunk table (RenderChunk.obj is group-relative), so
+// no workgroup touches another group's rays.
+__global__ __launch_bounds__(RENDER_RAYS) void k_sample_scan(const RenderChunk* __restrict__ chunks,
+                                                             const ObjDesc* __restrict__ desc,
+                                                             const ObjState* __restrict__ st,
+                                                             const float* __restrict__ rays_all, int M,
+                                                             int* __restrict__ dead, int* __restrict__ rinfo) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  const ObjState& S = st[ch.obj];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[ch.obj];
+  __shared__ SampleLds L;
+  stage_samples(L, S, M, threadIdx.x);
+  __syncthreads();
+  const int ray = ch.ray0 + threadIdx.x;
+  if (ray >= d.n_rays) return;
+  const float* rays = rays_all + (size_t)d.ray_off * 3;
+  const float3 rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
+  dead_put(dead + d.ray_off + ray, 0);
+  int rank = 0, jf = -1, jl = -1;
+  for (int j = 0; j < M; ++j) {
+    const float3 x = ray_sample(rv, L, j);
+    const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+    if (!(nrm < 1.0f)) continue;
+    if (jf < 0) jf = j;
+    jl = j;
+    ++rank;
+  }
+  rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
+}
+
+// prescanned: the first pass's runs and dead flags come from k_sample_scan
 __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
                                                                 ObjState* st, const float* __restrict__ rays_all,
                                                                 int M, int ra, int rb, float4* __restrict__ cand,
                                                                 float* __restrict__ dense, int* __restrict__ dead,
-                                                                int* __restrict__ rinfo) {
+                                                                int* __restrict__ rinfo, int prescanned) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -369,9 +405,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
     float3 rv = make_float3(0.f, 0.f, 0.f);
     if (ray < d.n_rays) {
       rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
-      if (first) dead[d.ray_off + ray] = 0;
-      alive = first || dead[d.ray_off + ray] == 0;
-      if (alive && !first) {
+      if (first && !prescanned) dead_put(dead + d.ray_off + ray, 0);
+      alive = first || dead_get(dead + d.ray_off + ray) == 0;
+      if (alive && (!first || prescanned)) {
         const int info = rinfo[d.ray_off + ray];
         if (info >= 0) {          // contiguous in-ball run (first pass): the window directly
           j0 = info & 255;
@@ -394,7 +430,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
         nin = rank;
         // the in-ball set of a ray is one run of samples unless rounding makes |x| < 1
         // flicker near a tangent point; such rays keep scanning in every pass
-        if (first)
+        if (first && !prescanned)
           rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
       }
     }
@@ -756,7 +792,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd(DevDecoder D, const Tile* __res
       const float y = tanhf(s + D.b8);
       const int idx = __float_as_int(sm.xyz[tid * 4 + 3]) & ~AUDIT_BIT;   // (audit tag: lite_flag)
       dense[d.cand_off + idx] = y;
-      if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;
+      if (E.dead && y <= E.nth) dead_put(E.dead + d.ray_off + idx / E.M, 1);
     }
     __syncthreads();
   }
@@ -1626,6 +1662,10 @@ __device__ __forceinline__ float quad_bcast(float v, int k) {
 // ------------------------------------------------------------------------------------
 constexpr int SOLVE_THREADS = 320;   // 5 waves: substitutions run 4 lanes per column
 constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render, T, z
+// trace records per (iteration, object), each a whole number of 128 B lines (like counts)
+constexpr int TRACE_H_STRIDE = (NPAR * NPAR + 31) / 32 * 32;
+constexpr int TRACE_V_STRIDE = (TRACE_V + 31) / 32 * 32;
+constexpr int TRACE_I_STRIDE = 32;
 
 // k_reduce_slots: the per-tile normal-equation partials of each object summed in tile order
 // (sdf tiles, render tiles: two fp64 sums per element, rounded once), one thread per element
@@ -1636,6 +1676,10 @@ constexpr int TRACE_V = 2 * NPAR + 3 + 16 + CODE;   // b, dx, loss, sdf, render,
 // (counts[it][o][NCOUNT], dsr_batch_stats) before k_solve may end the object.
 constexpr int SLOT_BLOCKS = (SLOT_FLOATS + 255) / 256;
 constexpr int NCOUNT = 6;
+// Per-object records written by concurrently running object groups start on their own 128 B
+// line: counts[it][o] is one line, red[o] a whole number of lines.
+constexpr int COUNT_STRIDE = 32;
+constexpr int SRED_STRIDE = (2 * SLOT_FLOATS + 31) / 32 * 32;
 
 __global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict__ desc,
                                                       const ObjState* __restrict__ st,
@@ -1644,7 +1688,7 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict_
   const int o = blockIdx.x / SLOT_BLOCKS;
   const ObjState& S = st[o];
   if (blockIdx.x == o * SLOT_BLOCKS && threadIdx.x == 0) {
-    int* c = counts + ((size_t)it * stride + o) * NCOUNT;
+    int* c = counts + ((size_t)it * stride + o) * COUNT_STRIDE;
     if (S.status != ST_RUNNING) {               // finished / failed objects did no work
       for (int i = 0; i < NCOUNT; ++i) c[i] = 0;
     } else {
@@ -1676,8 +1720,8 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const ObjDesc* __restrict_
   };
   const float a = sum(S.n_sdf_tiles);
   const float b = sum(S.n_ren_tiles);
-  red[(size_t)o * 2 * SLOT_FLOATS + e] = a;
-  red[(size_t)o * 2 * SLOT_FLOATS + SLOT_FLOATS + e] = b;
+  red[(size_t)o * SRED_STRIDE + e] = a;
+  red[(size_t)o * SRED_STRIDE + SLOT_FLOATS + e] = b;
 }
 
 // Rotation prior (compute_rotation_loss_sim3, loss.py:169-192) at the pre-update pose: returns
@@ -1768,7 +1812,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   const long long tp0 = wall_clock64();
 #endif
   {   // the tile partials' sums (k_reduce_slots)
-    const float* r = red + (size_t)o * 2 * SLOT_FLOATS;
+    const float* r = red + (size_t)o * SRED_STRIDE;
     for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {
       Ss[e] = r[e];
       Sr[e] = r[SLOT_FLOATS + e];
@@ -1831,7 +1875,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __syncthreads();
   if (trace_H) {
     for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS)
-      trace_H[((size_t)it * stride + o) * NPAR * NPAR + e] = A[e / NPAR][e % NPAR];
+      trace_H[((size_t)it * stride + o) * TRACE_H_STRIDE + e] = A[e / NPAR][e % NPAR];
   }
   __syncthreads();
 #ifdef DSR_SOLVE_PROFILE
@@ -1983,7 +2027,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     S.iters_done = it + 1;
     if (it + 1 >= P.iters) S.status = ST_DONE;
     if (trace_v) {
-      float* tv = trace_v + ((size_t)it * stride + o) * TRACE_V;
+      float* tv = trace_v + ((size_t)it * stride + o) * TRACE_V_STRIDE;
       for (int i = 0; i < NPAR; ++i) { tv[i] = bv[i]; tv[NPAR + i] = dx[i]; }
       tv[2 * NPAR + 0] = scal[0];
       tv[2 * NPAR + 1] = S.sdf_loss;
@@ -1993,8 +2037,8 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     }
   }
   if (trace_i && tid == 0) {
-    trace_i[((size_t)it * stride + o) * 2 + 0] = S.n_valid;
-    trace_i[((size_t)it * stride + o) * 2 + 1] = S.k;
+    trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 0] = S.n_valid;
+    trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 1] = S.k;
   }
 }
 

@@ -995,7 +995,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd16(DevDecoder D, const Tile* __r
           }
           dense[d.cand_off + idx] = y;
           if constexpr (MSK) MA.yv[d.cand_off + tl.start + tid] = y;
-          if (E.dead && y <= E.nth) E.dead[d.ray_off + idx / E.M] = 1;   // occupancy 1: ray terminated
+          if (E.dead && y <= E.nth) dead_put(E.dead + d.ray_off + idx / E.M, 1);   // occupancy 1: ray terminated
         }
       }
       stamp(11);

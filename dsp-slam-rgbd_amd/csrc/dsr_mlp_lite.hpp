@@ -436,7 +436,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
         bool full = false;
         const unsigned char fl = ((LV & 8) && sm.ovf) ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
         if (fl) E.refine[d.cand_off + idx] = fl;                 // band / range guard / audit
-        if (fl != 1 && full) E.dead[d.ray_off + idx / E.M] = 1;  // certainly full
+        if (fl != 1 && full) dead_put(E.dead + d.ray_off + idx / E.M, 1);  // certainly full
       }
     }
     __syncthreads();
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
           const unsigned char fl = (sm.ovf[p] == it + 1 || sm.broken)
                                        ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
           if (fl) E.refine[d.cand_off + idx] = fl;               // band / range guard / audit
-          if (fl != 1 && full) E.dead[d.ray_off + idx / E.M] = 1;  // certainly full
+          if (fl != 1 && full) dead_put(E.dead + d.ray_off + idx / E.M, 1);  // certainly full
 #else
           if (y == 12345.f) dense[d.cand_off + idx] = margin;
 #endif
