@@ -1184,9 +1184,13 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
-  {   // DSR_PRESCAN (test hook): the first pass's ray scan as its own chunked launch
+  {
+    // The first pass's ray scan as its own chunked launch (k_sample_scan) for one-group batches
+    // — single calls, graph-mode keyframe slots — whose decode counts it leaves run-to-run
+    // identical; with 4 groups the counts varied, so multi-group batches keep
+    // the scan inside k_sample_pass.  DSR_PRESCAN=0/1 (test hook) forces it.
     const char* e = hook_env("DSR_PRESCAN");
-    b->prescan = e && atoi(e) != 0;
+    b->prescan = e ? atoi(e) != 0 : b->groups.size() == 1;
   }
   {
     // the lite pass runs only on decoders that passed their load-time qualification
