@@ -300,8 +300,18 @@ def test_default_schedules_give_bitwise_equal_results(gpu_decoder, monkeypatch):
     monkeypatch.setenv("DSR_TEST_HOOKS", "1")   # kernel switches are test hooks
     monkeypatch.setenv("DSR_RENDER_PASSES", "0")
     runs["one_pass"] = opt.reconstruct_objects(objs[:8], trace=True)
+    monkeypatch.delenv("DSR_RENDER_PASSES")
+    # the object groups' slices packed back to back instead of line-aligned;
+    # one group with the first pass's chunked ray scan (its default) and without it
+    monkeypatch.setenv("DSR_GROUP_ALIGN", "0")
+    runs["packed"] = opt.reconstruct_objects(objs[:8], trace=True)
+    monkeypatch.delenv("DSR_GROUP_ALIGN")
+    monkeypatch.setenv("DSR_STREAMS", "1")
+    runs["one_group_scan"] = opt.reconstruct_objects(objs[:8], trace=True)
+    monkeypatch.setenv("DSR_PRESCAN", "0")
+    runs["one_group_no_scan"] = opt.reconstruct_objects(objs[:8], trace=True)
     ref_res, ref_tr = runs["batch8"]
-    cases = [("batch16", runs["batch16"], range(8)), ("one_pass", runs["one_pass"], range(8))]
+    cases = [(k, runs[k], range(8)) for k in ("batch16", "one_pass", "packed", "one_group_scan", "one_group_no_scan")]
     cases += [(f"single{i}", singles[i], [i]) for i in range(len(singles))]
     for name, (res, tr), idx in cases:
         for j, i in enumerate(idx):
