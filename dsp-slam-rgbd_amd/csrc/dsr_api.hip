@@ -914,13 +914,15 @@ int dsr_decoder_free(dsr_ctx* ctx, dsr_decoder* dec) {
 // Redwood object per reconstruct_object call 4.1 -> 3.1 ms; a KITTI object, 112k samples, 9.8 ms
 // either way; the 8-hypothesis keyframe batch 4.90 ms with 16,24 vs 5.90 with one pass).
 // A batch whose first 16-rank window would spill just past one round of lite tiles (n_cu
-// 128-point tiles: one KITTI-sized object per call) gets a first window that fits that round.
+// 128-point tiles: one KITTI-sized object per call) runs TWO passes, ranks [0, 20) and the rest:
+// one KITTI object per call 8.14 ms with round 4's round-filling first window (14,24), 7.88 with
+// 20 (24: 7.91, 16: 8.76, one pass 8.77; r5bb, 40 calls each, same box).
 static std::vector<int> render_passes(int M, long samples, long rays, int n_cu) {
   const char* e = hook_env("DSR_RENDER_PASSES");
   std::string spec = e ? e : (samples >= 1000000 ? "8,12,16,20,24,32" : samples >= 100000 ? "16,24" : "0");
   const long round = (long)n_cu * LTILE;
   if (!e && spec == "16,24" && rays > 0 && rays * 16 > round && rays * 12 <= round)
-    spec = std::to_string(round / rays) + ",24";
+    spec = "20";
   std::vector<int> r{0};
   size_t p = 0;
   while (p < spec.size()) {

@@ -283,7 +283,7 @@ def test_batch_equals_single(gpu_decoder, streams, monkeypatch):
 def test_default_schedules_give_bitwise_equal_results(gpu_decoder, monkeypatch):
     """the default render-pass schedule depends on the batch's sample
     count, ray count and the device's CU count — so an object alone (one KITTI object: windows
-    14,24), in an 8-object shard (16,24), in a 16-object frame (8,12,16,20,24,32) or decoded in
+    20), in an 8-object shard (16,24), in a 16-object frame (8,12,16,20,24,32) or decoded in
     ONE pass gets a different schedule.  None of this may change a bit of its result: the lite
     values are per sample, every sample in front of a ray's first certainly-full one is decoded
     under every schedule, and the exact pass re-decodes exactly those flagged in front of it
