@@ -34,6 +34,7 @@ Usage: python bench.py [--gpus N --steps K --warmup W --objects B --pts P --weak
 from __future__ import annotations
 
 import argparse
+import contextlib
 import ctypes as C
 import json
 import os
@@ -165,6 +166,22 @@ def pmc_traffic(kernel):
             if kernel in name and "hbm_bytes_per_launch" in e:
                 best = (e["hbm_bytes_per_launch"], os.path.relpath(f, REPO))
     return best
+
+
+@contextlib.contextmanager
+def env_set(**kv):
+    """The bench legs' environment switches, restored on the way out even when a leg raises
+    (a failed fp32 leg must not leave the later legs on the fp32 kernels)."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update(kv)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def stats_sum(acc, st):
@@ -660,37 +677,35 @@ def main():
             out["config4"] = c4
     if world == 1 and not args.no_extra:
         # exact-decode leg: DSR_LITE=0 (every in-ball sample decoded in 3xFP16), same job
-        os.environ["DSR_LITE"] = "0"
-        ex = ResidentShard(opt, objs)
-        ex.run()
-        torch.cuda.synchronize()
         k = min(args.steps, 3)
-        t1 = time.perf_counter()
-        for _ in range(k):
+        with env_set(DSR_LITE="0"):
+            ex = ResidentShard(opt, objs)
             ex.run()
-        dt = time.perf_counter() - t1
-        ex.close()
-        del os.environ["DSR_LITE"]
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(k):
+                ex.run()
+            dt = time.perf_counter() - t1
+            ex.close()
         out["value_exact"] = n_job * k / dt
         out["value_exact_note"] = "DSR_LITE=0: no classification pass, every in-ball sample decoded exactly"
         # fp32-arithmetic leg: the same job with the exact pass and the
         # Jacobian on the fp32-MFMA kernels (test hooks DSR_FWD_VARIANT / DSR_JAC_VARIANT 0; the
         # lite classification stays fp16): what fp32 arithmetic costs, and those kernels' rate
         # against the 157.3 TF fp32 MFMA peak
-        hooks = {"DSR_TEST_HOOKS": "1", "DSR_FWD_VARIANT": "0", "DSR_JAC_VARIANT": "0"}
-        os.environ.update(hooks)
-        f32 = ResidentShard(opt, objs)
-        f32.run()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(k):
-            f32.run()
-        dt = time.perf_counter() - t1
-        st32 = L.Stats()
-        ctx.check(lib.dsr_batch_stats(f32.handle, C.byref(st32)), "stats")
-        f32.close()
-        for key in hooks:
-            del os.environ[key]
+        with env_set(DSR_TEST_HOOKS="1", DSR_FWD_VARIANT="0", DSR_JAC_VARIANT="0"):
+            f32 = ResidentShard(opt, objs)
+            try:
+                f32.run()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(k):
+                    f32.run()
+                dt = time.perf_counter() - t1
+                st32 = L.Stats()
+                ctx.check(lib.dsr_batch_stats(f32.handle, C.byref(st32)), "stats")
+            finally:
+                f32.close()
         a32 = stats_sum({}, st32)
         out["fp32_leg"] = {"value": n_job * k / dt, "unit": "objects/s",
                            "fwd_variant": a32.get("fwd_variant"), "jac_variant": a32.get("jac_variant"),
@@ -702,14 +717,15 @@ def main():
         # the three MFMA kernels with the job on ONE stream: per-launch rates without the other
         # object group's concurrent kernels inside each launch's duration; the
         # headline roofline above is the timed region's, with both groups overlapping
-        os.environ["DSR_STREAMS"] = "1"
-        one = ResidentShard(opt, objs)
-        one.run()
-        one.run()
-        st1 = L.Stats()
-        ctx.check(lib.dsr_batch_stats(one.handle, C.byref(st1)), "stats")
-        one.close()
-        del os.environ["DSR_STREAMS"]
+        with env_set(DSR_STREAMS="1"):
+            one = ResidentShard(opt, objs)
+            try:
+                one.run()
+                one.run()
+                st1 = L.Stats()
+                ctx.check(lib.dsr_batch_stats(one.handle, C.byref(st1)), "stats")
+            finally:
+                one.close()
         r1 = kernel_rooflines(stats_sum({}, st1))
         out["rooflines_one_stream"] = {name: {k2: e[k2] for k2 in ("achieved_tflops", "peak_tflops", "frac_of_peak",
                                                                    "avg_launch_ms", "launches")}

@@ -161,6 +161,16 @@ static int lite_variant() {
   const char* e = hook_env("DSR_LITE_VARIANT");
   return e ? atoi(e) : DSR_DEFAULT_LITE_VARIANT;
 }
+// the lite variant lite_kernel() dispatches for the environment's setting (unknown numbers run 1496)
+static int lite_variant_dispatched() {
+  switch (lite_variant()) {
+#ifdef DSR_LITE_EXPERIMENTS
+    case 18: case 984: case 216: case 16: case 32: case 40: case 48: case 56: case 24: case 88:
+#endif
+    case 472: return lite_variant();
+  }
+  return 1496;
+}
 static LiteKernel lite_kernel() {
   switch (lite_variant()) {
 #ifdef DSR_LITE_EXPERIMENTS
@@ -293,6 +303,19 @@ struct dsr_batch {
   int runs = 0;
   bool timed = false;               // last run recorded per-kernel events (eager run)
   bool prescan = false;             // first pass's ray scan over the ray chunks (k_sample_scan)
+  // the kernels the last enqueue dispatched (dsr_stats, ABI 11; resolved there, so a later change
+  // of the environment cannot misreport them)
+  int ran_fwd = 0, ran_jac = 0, ran_lite = 0, ran_ring = 0;
+#ifdef DSR_EXP_PROV
+  int *prov_alive = nullptr, *prov_set = nullptr, *prov_xcc = nullptr, *prov_j = nullptr;   // (PROV_IT)
+  unsigned* prov_t = nullptr;
+  unsigned* prov_h = nullptr;
+  unsigned* prov_ri = nullptr;
+  float* prov_nrm = nullptr;
+  float* prov_nrm2 = nullptr;
+  float* prov_y = nullptr;
+  int prov_R = 0, prov_C = 0;
+#endif
   hipGraphExec_t graph = nullptr;   // the whole run, captured on the 2nd dsr_batch_run
   long graph_key = -1;              // kernel variants the graph was captured with
   int captures = 0, replays = 0;    // graph captures / replays over the batch's life
@@ -1186,11 +1209,71 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
+#ifdef DSR_EXP_PROV
+  {
+    int* pa = nullptr;
+    float* py = nullptr;
+    int* ps = nullptr;
+    int* px = nullptr;
+    const int R = std::max(1, ray_off), C = std::max(1, cand_off);
+    int* pj = nullptr;
+    unsigned* pt = nullptr;
+    ALLOC(pj, sizeof(int) * (size_t)PROV_IT * 64 * R);
+    ALLOC(pt, sizeof(unsigned) * (size_t)PROV_IT * 65 * R);
+    hipMemset(pj, 0xff, sizeof(int) * (size_t)PROV_IT * 64 * R);
+    hipMemset(pt, 0xff, sizeof(unsigned) * (size_t)PROV_IT * 65 * R);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_j), &pj, sizeof(pj));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_t), &pt, sizeof(pt));
+    b->prov_j = pj;
+    b->prov_t = pt;
+    float* pn2 = nullptr;
+    ALLOC(pn2, sizeof(float) * (size_t)PROV_IT * R * 8);
+    hipMemset(pn2, 0, sizeof(float) * (size_t)PROV_IT * R * 8);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_nrm2), &pn2, sizeof(pn2));
+    b->prov_nrm2 = pn2;
+    float* pn = nullptr;
+    ALLOC(pn, sizeof(float) * (size_t)PROV_IT * R * 12);
+    hipMemset(pn, 0, sizeof(float) * (size_t)PROV_IT * R * 12);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_nrm), &pn, sizeof(pn));
+    b->prov_nrm = pn;
+    unsigned* pr = nullptr;
+    ALLOC(pr, sizeof(unsigned) * 2 * (size_t)PROV_IT * R * 2);
+    hipMemset(pr, 0, sizeof(unsigned) * 2 * (size_t)PROV_IT * R * 2);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_ri), &pr, sizeof(pr));
+    b->prov_ri = pr;
+    unsigned* ph = nullptr;
+    ALLOC(ph, sizeof(unsigned) * 2 * (size_t)PROV_IT * R * 3);
+    hipMemset(ph, 0, sizeof(unsigned) * 2 * (size_t)PROV_IT * R * 3);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_h), &ph, sizeof(ph));
+    b->prov_h = ph;
+    ALLOC(px, sizeof(int) * (size_t)PROV_IT * R * 2);
+    hipMemset(px, 0xff, sizeof(int) * (size_t)PROV_IT * R * 2);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_xcc), &px, sizeof(px));
+    b->prov_xcc = px;
+    ALLOC(pa, sizeof(int) * (size_t)PROV_IT * 64 * R);
+    ALLOC(py, sizeof(float) * (size_t)PROV_IT * C);
+    ALLOC(ps, sizeof(int) * (size_t)PROV_IT * R);
+    hipMemset(pa, 0, sizeof(int) * (size_t)PROV_IT * 64 * R);
+    hipMemset(py, 0xff, sizeof(float) * (size_t)PROV_IT * C);
+    hipMemset(ps, 0x7f, sizeof(int) * (size_t)PROV_IT * R);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_alive), &pa, sizeof(pa));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_y), &py, sizeof(py));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_set), &ps, sizeof(ps));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_R), &R, sizeof(R));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prov_C), &C, sizeof(C));
+    b->prov_alive = pa;
+    b->prov_y = py;
+    b->prov_set = ps;
+    b->prov_R = R;
+    b->prov_C = C;
+  }
+#endif
   {
     // The first pass's ray scan as its own chunked launch (k_sample_scan) for one-group batches
-    // — single calls, graph-mode keyframe slots — whose decode counts it leaves run-to-run
-    // identical; with 4 groups the counts varied, so multi-group batches keep
-    // the scan inside k_sample_pass.  DSR_PRESCAN=0/1 (test hook) forces it.
+    // — single calls, graph-mode keyframe slots — where it takes ~0.3 ms off a KITTI object's call.
+    // Its round-4/5 timing-dependent decode counts were wrong products of a packed-FP32 multiply
+    // in its loop's first trip; the kernel is built without packed FP32 now.
+    // DSR_PRESCAN=0/1 (test hook) forces it.
     const char* e = hook_env("DSR_PRESCAN");
     b->prescan = e ? atoi(e) != 0 : b->groups.size() == 1;
   }
@@ -1592,6 +1675,16 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
   const FwdKernel fwdk = fwd_kernel_for(D, fv);
   const JacKernel jack = jac_kernel_for(D);
   const LiteKernel litek = lite_kernel();
+  // (the kernels dispatched, as dsr_batch_stats reports them: fwd_kernel / jac_kernel's choice)
+  {
+    const int fl = fv & 15;
+    const bool known = fl == 1 || fl == 2 || fl == 3 || fl == 6 || fl == 7 || fl == 8 || fl == 12;
+    const int jv = jac_variant();
+    b->ran_fwd = is_variant(D) ? 12 : (known ? fv : (fv & ~15));
+    b->ran_jac = is_variant(D) ? 12 : ((jv == 8 || jv == 12) ? jv : 0);
+    b->ran_lite = b->lite ? lite_variant_dispatched() : 0;
+    b->ran_ring = is_variant(D) ? 2 : split_ring();
+  }
   const int np = (int)b->passes.size() - 1;
   const size_t epi = ev_per_iter(b);
   const int G = (int)b->groups.size();
@@ -1619,13 +1712,17 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
                                        (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       const bool pre = b->prescan && gr.n_rch > 0;
+      int pre_arg = pre ? 1 : 0;                 // k_sample_pass's `prescanned` for the first pass
+#ifdef DSR_EXP_PROV
+      if (pre && getenv("DSR_EXP_SCAN_NOCLEAR")) pre_arg = 3;   // the scan writes the runs only
+#endif
       if (pre)                                   // the first pass's ray scan over the ray chunks
         hipLaunchKernelGGL(k_sample_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                           b->M, b->dead, b->rinfo);
+                           b->M, pre_arg == 3 ? (int*)nullptr : b->dead, b->rinfo);
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                            b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo,
-                           (pz == 0 && pre) ? 1 : 0);
+                           pz == 0 ? pre_arg : 0);
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
                            b->lite ? LTILE : TILE, 0);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
@@ -1764,17 +1861,18 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   st->graph_replays = b->replays;
   st->n_groups = (int)b->groups.size();
   st->graph_mode = b->cap_graph ? 2 : (graph_enabled() ? 1 : 0);
-  st->fwd_variant = fwd_variant();
-  st->jac_variant = jac_variant();
-  st->lite_variant = b->lite ? lite_variant() : 0;
-  st->split_ring = split_ring();
+  st->fwd_variant = b->ran_fwd;
+  st->jac_variant = b->ran_jac;
+  st->lite_variant = b->ran_lite;
+  st->split_ring = b->ran_ring;
+  st->prescan = b->prescan ? 1 : 0;
   {
     int nb = 0;
     DSR_CHECK(b->ctx, hipMemcpy(&nb, b->diag + STD_BROKEN, sizeof(int), hipMemcpyDeviceToHost));
     st->lite_broken_blocks = nb;
   }
-  st->keep_masks = (b->lite && b->ma.msk && fwd_variant() == 12) ? 1 : 0;
-  st->surface_in_exact = (st->keep_masks && b->ma.pts && jac_variant() == 12) ? 1 : 0;
+  st->keep_masks = (b->lite && b->ma.msk && b->ran_fwd == 12) ? 1 : 0;
+  st->surface_in_exact = (st->keep_masks && b->ma.pts && b->ran_jac == 12) ? 1 : 0;
   if (b->lite) {
     st->lite_min_margin = 1e30;
     for (const ObjState& o : hs) {
@@ -1800,6 +1898,32 @@ int dsr_batch_stats(dsr_batch* b, dsr_stats* st) {
   return 0;
 }
 
+#ifdef DSR_EXP_PROV
+// diagnostic build only: the provenance arrays of the batch's last run (tools/prov_diff.py);
+// null pointers: just the sizes R (rays) and C (samples)
+int dsr_exp_prov(dsr_batch* b, int* alive, float* y, int* set, int* xcc, int* R, int* C, int* jf, unsigned* t,
+                 unsigned* h, unsigned* ri, float* nrm, float* nrm2) {
+  if (!b) return -2;
+  hipSetDevice(b->ctx->device);
+  if (b->ran) {
+    const int rc = batch_finish(b);
+    if (rc) return rc;
+  }
+  if (R) *R = b->prov_R;
+  if (C) *C = b->prov_C;
+  if (alive) DSR_CHECK(b->ctx, hipMemcpy(alive, b->prov_alive, sizeof(int) * (size_t)PROV_IT * 64 * b->prov_R, hipMemcpyDeviceToHost));
+  if (y) DSR_CHECK(b->ctx, hipMemcpy(y, b->prov_y, sizeof(float) * (size_t)PROV_IT * b->prov_C, hipMemcpyDeviceToHost));
+  if (nrm2) DSR_CHECK(b->ctx, hipMemcpy(nrm2, b->prov_nrm2, sizeof(float) * (size_t)PROV_IT * b->prov_R * 8, hipMemcpyDeviceToHost));
+  if (nrm) DSR_CHECK(b->ctx, hipMemcpy(nrm, b->prov_nrm, sizeof(float) * (size_t)PROV_IT * b->prov_R * 12, hipMemcpyDeviceToHost));
+  if (ri) DSR_CHECK(b->ctx, hipMemcpy(ri, b->prov_ri, sizeof(unsigned) * 2 * (size_t)PROV_IT * b->prov_R * 2, hipMemcpyDeviceToHost));
+  if (h) DSR_CHECK(b->ctx, hipMemcpy(h, b->prov_h, sizeof(unsigned) * 2 * (size_t)PROV_IT * b->prov_R * 3, hipMemcpyDeviceToHost));
+  if (jf) DSR_CHECK(b->ctx, hipMemcpy(jf, b->prov_j, sizeof(int) * (size_t)PROV_IT * 64 * b->prov_R, hipMemcpyDeviceToHost));
+  if (t) DSR_CHECK(b->ctx, hipMemcpy(t, b->prov_t, sizeof(unsigned) * (size_t)PROV_IT * 65 * b->prov_R, hipMemcpyDeviceToHost));
+  if (xcc) DSR_CHECK(b->ctx, hipMemcpy(xcc, b->prov_xcc, sizeof(int) * (size_t)PROV_IT * b->prov_R * 2, hipMemcpyDeviceToHost));
+  if (set) DSR_CHECK(b->ctx, hipMemcpy(set, b->prov_set, sizeof(int) * (size_t)PROV_IT * b->prov_R, hipMemcpyDeviceToHost));
+  return 0;
+}
+#endif
 int dsr_batch_lite_diag(dsr_batch* b, int* rec, int n) {
   if (!b || !rec || n < 0) return -2;
   if (!b->ran) return fail(b->ctx, "batch has not run");
@@ -1893,6 +2017,8 @@ int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_
           if (t.z) std::memcpy(t.z + (size_t)e * dec->code_len, v + 2 * NPAR + 19, sizeof(float) * dec->code_len);
           if (t.n_valid) t.n_valid[e] = I[k * TRACE_I_STRIDE];
           if (t.k) t.k[e] = I[k * TRACE_I_STRIDE + 1];
+          if (t.n_decoded) t.n_decoded[e] = I[k * TRACE_I_STRIDE + 2];
+          if (t.n_refined) t.n_refined[e] = I[k * TRACE_I_STRIDE + 3];
         }
       }
     }

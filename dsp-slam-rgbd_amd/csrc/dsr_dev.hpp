@@ -81,10 +81,11 @@ struct DevDecoder {
 // normalised activations x^ (acc layout, [16 (q, cb)][512 threads] float4) and rstd per point,
 // written by the forward and read back by the backward of the same tile
 constexpr int LN_WS_LAYER = 16 * 512 * 4 + 64;     // floats
-constexpr int LN_WS_WG = 8 * LN_WS_LAYER;          // floats per workgroup (4.2 MB: 8 layers x 16 float4
-                                                   // x 512 threads + rstd); n_cu of them per stream, so
-                                                   // ~1.3 GB per object-group stream on 304 CUs, allocated
-                                                   // only for LayerNorm decoders (never DSP-SLAM's)
+constexpr int LN_WS_WG = 8 * LN_WS_LAYER;          // floats per workgroup (262,656 floats = 1.05 MB:
+                                                   // 8 layers x (16 float4 x 512 threads + rstd)); n_cu
+                                                   // of them per stream, so ~270 MB per object-group
+                                                   // stream on MI355X's 256 CUs, allocated only for
+                                                   // LayerNorm decoders (never DSP-SLAM's)
 
 // row of the point's xyz in the input of the layer after lin_l (l = 0..7), or -1: lin4's input
 // is [h3 | code (folded) | xyz] (row l3), with xyz_in_all every other layer's is [h | xyz] (509)
@@ -94,6 +95,14 @@ __device__ __forceinline__ int xyz_row(const DevDecoder& D, int l) {
 
 // d sdf / d[code, xyz] slot (gin, 64-D layout: code 0..63, xyz 64..66) of lin4's input row n >= l3
 __device__ __forceinline__ int gin_slot(int n, int l3) { return n < HID - 3 ? n - l3 : CODE + (n - (HID - 3)); }
+
+// Kernels built without packed-FP32 VALU instructions (v_pk_mul/add/fma_f32): DESIGN.md §3.9.
+// DSR_EXP_PKSCAN (diagnostic builds) keeps them, to reproduce the round-6 finding.
+#ifdef DSR_EXP_PKSCAN
+#define DSR_NO_PK_F32
+#else
+#define DSR_NO_PK_F32 __attribute__((target("no-packed-fp32-ops")))
+#endif
 
 struct ObjDesc {
   int pts_off, n_pts;    // into pts
@@ -154,6 +163,73 @@ __device__ __forceinline__ int dead_get(int* p) {
   return *p;
 #endif
 }
+#ifdef DSR_EXP_PROV
+// Diagnostic build only (tools/prov_diff.py): per-run provenance of the early
+// ray termination — for every (iteration, pass start rank, ray) whether k_sample_pass found the
+// ray alive and how many samples it emitted, for every (iteration, sample) the lite value, and
+// for every (iteration, ray) the first depth index whose lite value terminated it.
+constexpr int PROV_IT = 12;
+__device__ int* g_prov_alive;   // [PROV_IT][64][R]: cnt + 1 (alive), -1 (dead), 0 (not visited)
+__device__ float* g_prov_y;     // [PROV_IT][C]: lite value (NaN: not decoded)
+__device__ int* g_prov_set;     // [PROV_IT][R]: smallest j that set the dead flag (INT_MAX: none)
+__device__ int* g_prov_xcc;     // [PROV_IT][R][2]: XCC of the workgroup that cleared / set the flag
+__device__ int* g_prov_j;       // [PROV_IT][64][R]: first depth index emitted by the pass (-1: none)
+__device__ unsigned* g_prov_t;  // [PROV_IT][65][R]: s_memrealtime (low 32 bits) of each pass's read
+                                // of the flag (rows 0..63) and of the first set (row 64)
+__device__ unsigned* g_prov_h;  // [2][PROV_IT][R][3]: (checksum of the object's pose T[0..11] and depths,
+                                // s_memrealtime, XCC) as k_iter_begin wrote them (row 0, key: the
+                                // object's first ray) and as each k_sample_scan chunk staged them
+                                // (row 1, key: the chunk's first ray)
+__device__ int g_prov_R, g_prov_C;
+__device__ float* g_prov_nrm2;  // [PROV_IT][R][8]: the same check in k_sample_pass's first-pass scan
+__device__ float* g_prov_nrm;   // [PROV_IT][R][12]: k_sample_scan's |x| of samples 0..3 in its loop,
+                                // recomputed after it, and the LDS depths 0..3 re-read after it
+__device__ unsigned* g_prov_ri; // [2][PROV_IT][R][2]: (rinfo value, s_memrealtime) as k_sample_scan wrote it
+                                // (row 0) and as the first k_sample_pass read it (row 1)
+__device__ inline void prov_rinfo(int row, int it, int ray, int v) {
+  if (!g_prov_ri || it >= PROV_IT) return;
+  unsigned* p = g_prov_ri + (((size_t)row * PROV_IT + it) * g_prov_R + ray) * 2;
+  p[0] = (unsigned)v;
+  p[1] = (unsigned)__builtin_amdgcn_s_memrealtime();
+}
+__device__ inline unsigned prov_sum(const float* T, const float* dep, int M) {
+  unsigned h = 0;
+  for (int i = 0; i < 12; ++i) h += __float_as_uint(T[i]) * (2u * i + 1u);
+  for (int i = 0; i < M; ++i) h += __float_as_uint(dep[i]) * (2u * i + 25u);
+  return h;
+}
+__device__ inline void prov_state(int row, int it, int key, unsigned h) {
+  if (!g_prov_h || it >= PROV_IT) return;
+  unsigned* p = g_prov_h + (((size_t)row * PROV_IT + it) * g_prov_R + key) * 3;
+  p[0] = h;
+  p[1] = (unsigned)__builtin_amdgcn_s_memrealtime();
+  p[2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+}
+__device__ inline unsigned prov_now() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
+__device__ inline void prov_emit(int it, int ra, int ray, int j) {
+  if (!g_prov_j || it >= PROV_IT || ra >= 64) return;
+  g_prov_j[((size_t)it * 64 + ra) * g_prov_R + ray] = j;
+  g_prov_t[((size_t)it * 65 + ra) * g_prov_R + ray] = prov_now();
+}
+__device__ inline int prov_xcc() { return (int)__builtin_amdgcn_s_getreg((31 << 11) | 20); }
+// alive entries: (cnt + 1 | -1) + 1024 * the reading workgroup's XCC
+__device__ inline void prov_alive(int it, int ra, int ray, int v) {
+  if (g_prov_alive && it < PROV_IT && ra < 64)
+    g_prov_alive[((size_t)it * 64 + ra) * g_prov_R + ray] = v + 1024 * prov_xcc();
+}
+__device__ inline void prov_clear(int it, int ray) {
+  if (g_prov_xcc && it < PROV_IT) g_prov_xcc[((size_t)it * g_prov_R + ray) * 2] = prov_xcc();
+}
+__device__ inline void prov_lite(int it, int sample, int ray, int j, float y, bool sets_dead) {
+  if (!g_prov_y || it >= PROV_IT) return;   // (decoder qualification, sdf queries: no batch)
+  g_prov_y[(size_t)it * g_prov_C + sample] = y;
+  if (sets_dead) {
+    atomicMin(g_prov_set + (size_t)it * g_prov_R + ray, j);
+    atomicMin(g_prov_t + ((size_t)it * 65 + 64) * g_prov_R + ray, prov_now());
+    g_prov_xcc[((size_t)it * g_prov_R + ray) * 2 + 1] = prov_xcc();
+  }
+}
+#endif
 struct ObjState;
 struct ErtArgs {
   int* dead;             // [sum n_rays] (nullptr: no flagging, e.g. dsr_sdf_eval)

@@ -274,6 +274,9 @@ __global__ __launch_bounds__(512) void k_iter_begin(int n_obj, const ObjDesc* __
       const float m = fmaxf(P.lite_floor, P.lite_safety * S.lite_err);
       S.lite_margin = (m <= 0.1f) ? m : 1e30f;          // beyond: every sample exact
     }
+#ifdef DSR_EXP_PROV
+    prov_state(0, S.iters_done, desc[o].ray_off, prov_sum(S.T, S.depths, M));
+#endif
   }
   __syncthreads();
   const ObjDesc d = desc[o];
@@ -348,7 +351,10 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 // the first window from the runs as later passes do.  Launched per object group with the
 // group's own descriptor / state slices and chunk table (RenderChunk.obj is group-relative), so
 // no workgroup touches another group's rays.
-__global__ __launch_bounds__(RENDER_RAYS) void k_sample_scan(const RenderChunk* __restrict__ chunks,
+// (no packed-FP32 VALU ops in this kernel, nor in the other two that form ray samples,
+// k_sample_pass and k_refine_emit: DESIGN.md §3.9 — under concurrent decoder kernels the
+// SLP-paired v_pk_mul_f32 of this loop's first trip returned wrong products in one quarter-wave)
+__global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_scan(const RenderChunk* __restrict__ chunks,
                                                              const ObjDesc* __restrict__ desc,
                                                              const ObjState* __restrict__ st,
                                                              const float* __restrict__ rays_all, int M,
@@ -360,25 +366,54 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_sample_scan(const RenderChunk* 
   __shared__ SampleLds L;
   stage_samples(L, S, M, threadIdx.x);
   __syncthreads();
+#ifdef DSR_EXP_PROV
+  if (threadIdx.x == 0) prov_state(1, S.iters_done, d.ray_off + ch.ray0, prov_sum(L.T, L.depths, M));
+#endif
   const int ray = ch.ray0 + threadIdx.x;
   if (ray >= d.n_rays) return;
   const float* rays = rays_all + (size_t)d.ray_off * 3;
   const float3 rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
-  dead_put(dead + d.ray_off + ray, 0);
+  if (dead) {                     // (nullptr: k_sample_pass clears the flags, DSR_EXP_SCAN_NOCLEAR)
+    dead_put(dead + d.ray_off + ray, 0);
+#ifdef DSR_EXP_PROV
+    prov_clear(S.iters_done, d.ray_off + ray);
+#endif
+  }
   int rank = 0, jf = -1, jl = -1;
+#ifdef DSR_EXP_PROV
+  float pn[4] = {0.f, 0.f, 0.f, 0.f};
+#endif
   for (int j = 0; j < M; ++j) {
     const float3 x = ray_sample(rv, L, j);
     const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+#ifdef DSR_EXP_PROV
+    if (j < 4) pn[j] = nrm;
+#endif
     if (!(nrm < 1.0f)) continue;
     if (jf < 0) jf = j;
     jl = j;
     ++rank;
   }
+#ifdef DSR_EXP_PROV
+  if (g_prov_nrm && S.iters_done < PROV_IT) {
+    float* q = g_prov_nrm + ((size_t)S.iters_done * g_prov_R + d.ray_off + ray) * 12;
+    for (int j = 0; j < 4; ++j) {
+      const float3 x = ray_sample(rv, L, j);
+      q[j] = pn[j];
+      q[4 + j] = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
+      q[8 + j] = L.depths[j];
+    }
+  }
+#endif
   rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
+#ifdef DSR_EXP_PROV
+  prov_rinfo(0, S.iters_done, d.ray_off + ray, rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1));
+#endif
 }
 
-// prescanned: the first pass's runs and dead flags come from k_sample_scan
-__global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
+// prescanned: bit 0 — the first pass's runs (and, without bit 1, its cleared dead flags) come
+// from k_sample_scan; bit 1 (diagnostic builds) — the first pass clears the flags itself
+__global__ __launch_bounds__(SAMPLE_THREADS) DSR_NO_PK_F32 void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
                                                                 ObjState* st, const float* __restrict__ rays_all,
                                                                 int M, int ra, int rb, float4* __restrict__ cand,
                                                                 float* __restrict__ dense, int* __restrict__ dead,
@@ -405,10 +440,18 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
     float3 rv = make_float3(0.f, 0.f, 0.f);
     if (ray < d.n_rays) {
       rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
-      if (first && !prescanned) dead_put(dead + d.ray_off + ray, 0);
+      if (first && (prescanned & 1) == (prescanned >> 1)) {   // 0 (no scan) or 3
+        dead_put(dead + d.ray_off + ray, 0);
+#ifdef DSR_EXP_PROV
+        prov_clear(S.iters_done, d.ray_off + ray);
+#endif
+      }
       alive = first || dead_get(dead + d.ray_off + ray) == 0;
       if (alive && (!first || prescanned)) {
         const int info = rinfo[d.ray_off + ray];
+#ifdef DSR_EXP_PROV
+        if (first) prov_rinfo(1, S.iters_done, d.ray_off + ray, info);
+#endif
         if (info >= 0) {          // contiguous in-ball run (first pass): the window directly
           j0 = info & 255;
           nin = info >> 8;
@@ -417,9 +460,15 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
       }
       if (alive && j0 < 0) {
         int rank = 0, jf = -1, jl = -1;
+#ifdef DSR_EXP_PROV
+        float pn[4] = {0.f, 0.f, 0.f, 0.f};
+#endif
         for (int j = 0; j < M; ++j) {
           const float3 x = ray_sample(rv, L, j);
           const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+#ifdef DSR_EXP_PROV
+          if (j < 4) pn[j] = nrm;
+#endif
           if (!(nrm < 1.0f)) continue;   // loss.py:82 (out of ball: NaN, dense pre-filled)
           if (jf < 0) jf = j;
           jl = j;
@@ -428,12 +477,28 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void k_sample_pass(int n_obj, const
           if (!first && rank >= rb) break;
         }
         nin = rank;
+#ifdef DSR_EXP_PROV
+        if (first && g_prov_nrm2 && S.iters_done < PROV_IT) {
+          float* q = g_prov_nrm2 + ((size_t)S.iters_done * g_prov_R + d.ray_off + ray) * 8;
+          for (int j = 0; j < 4; ++j) {
+            const float3 x = ray_sample(rv, L, j);
+            q[j] = pn[j];
+            q[4 + j] = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
+          }
+        }
+#endif
         // the in-ball set of a ray is one run of samples unless rounding makes |x| < 1
         // flicker near a tangent point; such rays keep scanning in every pass
         if (first && !prescanned)
           rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
       }
     }
+#ifdef DSR_EXP_PROV
+    if (ray < d.n_rays) {
+      prov_alive(S.iters_done, ra, d.ray_off + ray, alive ? cnt + 1 : -1);
+      prov_emit(S.iters_done, ra, d.ray_off + ray, cnt > 0 ? (j0 >= 0 ? j0 + ra : -2) : -1);
+    }
+#endif
     const int inc = wave_incl_scan(cnt, lane);
     int nin_w = nin;
 #pragma unroll
@@ -568,7 +633,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
   }
 }
 
-__global__ __launch_bounds__(RENDER_RAYS) void k_refine_emit(const RenderChunk* __restrict__ chunks,
+__global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_refine_emit(const RenderChunk* __restrict__ chunks,
                                                              const ObjDesc* __restrict__ desc, ObjState* st,
                                                              const float* __restrict__ rays_all, int M,
                                                              float4* __restrict__ cand, int* __restrict__ slotmap,
@@ -2039,6 +2104,8 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   if (trace_i && tid == 0) {
     trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 0] = S.n_valid;
     trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 1] = S.k;
+    trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 2] = S.n_eval;
+    trace_i[((size_t)it * stride + o) * TRACE_I_STRIDE + 3] = S.n_refine;
   }
 }
 

@@ -437,6 +437,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite(DevDecoder D, const Tile* 
         const unsigned char fl = ((LV & 8) && sm.ovf) ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
         if (fl) E.refine[d.cand_off + idx] = fl;                 // band / range guard / audit
         if (fl != 1 && full) dead_put(E.dead + d.ray_off + idx / E.M, 1);  // certainly full
+#ifdef DSR_EXP_PROV
+        prov_lite(So.iters_done, d.cand_off + idx, d.ray_off + idx / E.M, idx % E.M, y, fl != 1 && full);
+#endif
       }
     }
     __syncthreads();
@@ -851,6 +854,9 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_lite_st(DevDecoder D, const Til
                                        ? 1 : lite_flag(E, y, idx, margin, So.iters_done, full);
           if (fl) E.refine[d.cand_off + idx] = fl;               // band / range guard / audit
           if (fl != 1 && full) dead_put(E.dead + d.ray_off + idx / E.M, 1);  // certainly full
+#ifdef DSR_EXP_PROV
+          prov_lite(So.iters_done, d.cand_off + idx, d.ray_off + idx / E.M, idx % E.M, y, fl != 1 && full);
+#endif
 #else
           if (y == 12345.f) dense[d.cand_off + idx] = margin;
 #endif

@@ -65,10 +65,11 @@ class PoseIn(C.Structure):
 
 class Trace(C.Structure):
     _fields_ = [("H", FP), ("b", FP), ("dx", FP), ("loss", FP), ("sdf_loss", FP),
-                ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP)]
+                ("render_loss", FP), ("n_valid", IP), ("k", IP), ("t_obj_cam", FP), ("z", FP),
+                ("n_decoded", IP), ("n_refined", IP)]
 
 
-ABI_VERSION = 10         # include/dsr.h DSR_ABI_VERSION
+ABI_VERSION = 11         # include/dsr.h DSR_ABI_VERSION
 BATCH_GRAPH = 1          # include/dsr.h DSR_BATCH_GRAPH
 
 
@@ -87,7 +88,8 @@ class Stats(C.Structure):
                 ("audit_log2", C.c_int), ("lite_margin0", C.c_float), ("lite_floor", C.c_float),
                 ("lite_safety", C.c_float), ("graph_captures", C.c_int), ("graph_replays", C.c_int),
                 ("n_groups", C.c_int), ("graph_mode", C.c_int), ("fwd_variant", C.c_int),
-                ("jac_variant", C.c_int), ("lite_variant", C.c_int), ("split_ring", C.c_int)]
+                ("jac_variant", C.c_int), ("lite_variant", C.c_int), ("split_ring", C.c_int),
+                ("prescan", C.c_int)]
 
 
 class DecoderInfo(C.Structure):

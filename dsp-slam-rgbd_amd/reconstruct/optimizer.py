@@ -143,13 +143,14 @@ class Optimizer(object):
                          sdf_loss=np.zeros(it, np.float32), render_loss=np.zeros(it, np.float32),
                          n_valid=np.zeros(it, np.int32), k=np.zeros(it, np.int32),
                          t_obj_cam=np.zeros((it, 4, 4), np.float32),
-                         z=np.zeros((it, self.code_len), np.float32)) for _ in range(n)]
+                         z=np.zeros((it, self.code_len), np.float32),
+                         n_decoded=np.zeros(it, np.int32), n_refined=np.zeros(it, np.int32)) for _ in range(n)]
             tr = (L.Trace * n)()
             for i, bb in enumerate(bufs):
                 tr[i] = L.Trace(*(L.fptr(bb[k]) for k in ("H", "b", "dx", "loss", "sdf_loss",
                                                           "render_loss")),
                                 L.iptr(bb["n_valid"]), L.iptr(bb["k"]), L.fptr(bb["t_obj_cam"]),
-                                L.fptr(bb["z"]))
+                                L.fptr(bb["z"]), L.iptr(bb["n_decoded"]), L.iptr(bb["n_refined"]))
         t0 = time.time()
         ctx = self._ctx
         ctx.check(ctx.lib.dsr_reconstruct_batch(ctx.handle, self.decoder.handle,
@@ -207,7 +208,11 @@ class Optimizer(object):
     def _slot_for(self, objects):
         """A free fixed-capacity batch (dsr_batch_create_capacity) that holds ``objects``, or
         None (``keyframe_mode`` "oneshot", every slot busy with an in-flight keyframe, or no slot
-        within the capacity bounds above: the keyframe then runs as a one-shot batch)."""
+        within the capacity bounds above: the keyframe then runs as a one-shot batch).  A free
+        slot is grown (replaced by a larger one) only when the grown size stays inside the bounds;
+        otherwise the keyframe gets a slot of its own — beside the others while fewer than
+        MAX_SLOTS exist, else in place of the least recently used free slot (a small
+        keyframe no longer destroys a large free slot and its captured graph)."""
         if self.keyframe_mode not in ("slot", "graph") or not objects:
             return None
         n = len(objects)
@@ -216,24 +221,32 @@ class Optimizer(object):
         need_r = max(rays)
         real = sum(rays)
         graph = self.keyframe_mode == "graph"
+        self._slot_tick = getattr(self, "_slot_tick", 0) + 1
         free = [sl for sl in self._slots if not sl.busy and sl.graph == graph]
         for sl in free:
             if sl.fits(n, need_p, need_r) and self._slot_ok(sl.max_obj, sl.max_rays, real):
+                sl.last_used = self._slot_tick
                 return sl
         pad = lambda v: -(-v // 128) * 128  # noqa: E731
         cn, cp, cr = n, pad(need_p), pad(need_r)
-        if free:                                     # grow the first free slot, or replace it
-            old = free[0]
-            gn, gp, gr = max(cn, old.max_obj), max(cp, old.max_pts), max(cr, old.max_rays)
+        old = None
+        for sl in free:                              # grow a free slot inside the bounds
+            gn, gp, gr = max(cn, sl.max_obj), max(cp, sl.max_pts), max(cr, sl.max_rays)
             if self._slot_ok(gn, gr, real):
-                cn, cp, cr = gn, gp, gr
+                old, (cn, cp, cr) = sl, (gn, gp, gr)
+                break
+        if old is None:
+            if not self._slot_ok(cn, cr, real):
+                return None
+            if len(self._slots) >= self.MAX_SLOTS:   # evict the least recently used free slot
+                if not free:
+                    return None
+                old = min(free, key=lambda sl: getattr(sl, "last_used", 0))
+        if old is not None:
             self._slots.remove(old)
             old.close()
-        elif len(self._slots) >= self.MAX_SLOTS:
-            return None
-        if not self._slot_ok(cn, cr, real):
-            return None
         sl = SlotBatch(self, cn, cp, cr, graph)
+        sl.last_used = self._slot_tick
         self._slots.append(sl)
         return sl
 

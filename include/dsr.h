@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSR_ABI_VERSION 10
+#define DSR_ABI_VERSION 11
 #define DSR_MAX_LAYERS 16
 #define DSR_CODE_LEN 64
 
@@ -121,6 +121,11 @@ typedef struct {
   int* k;
   float* t_obj_cam;               /* [num_iterations][16] state the iteration started from */
   float* z;                       /* [num_iterations][code_len] */
+  /* ABI 11 (may be NULL): the iteration's work counts — ray samples decoded by the render passes
+     (early ray termination: every sample in front of a ray's first certainly-full one, plus
+     those its pass window held behind it) and samples re-decoded exactly after the lite pass */
+  int* n_decoded;
+  int* n_refined;
 } dsr_trace;
 
 typedef struct {
@@ -178,7 +183,11 @@ typedef struct {
   int lite_variant;               /* lite-pass kernel (1496 shipped; 0 when the lite pass is off) */
   int split_ring;                 /* A-ring depth of the split kernels (2 shipped).  Only under
                                      DSR_TEST_HOOKS=1 can DSR_FWD_VARIANT / _JAC_VARIANT /
-                                     _LITE_VARIANT / _SPLIT_RING move these from the shipped values */
+                                     _LITE_VARIANT / _SPLIT_RING move these from the shipped values.
+                                     ABI 11: the four are the kernels the last run DISPATCHED
+                                     (recorded as it was enqueued), not the environment's values */
+  int prescan;                    /* ABI 11: 1 if the first render pass's ray scan ran as its own
+                                     chunked launch (k_sample_scan; one-group batches) */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */

@@ -394,3 +394,35 @@ def test_query_never_waits_for_the_redo(gpu_decoder, monkeypatch):
     finally:
         lib.dsr_batch_destroy(h)
 
+
+
+def test_stats_report_the_kernels_the_run_dispatched(gpu_decoder, monkeypatch):
+    """dsr_stats' kernel fields (ABI 10/11) are the kernels the last run
+    dispatched, resolved as it was enqueued — an unknown DSR_LITE_VARIANT runs (and reports) the
+    shipped 1496, and changing the environment between run and stats changes nothing reported."""
+    from reconstruct import _libdsr as L
+
+    opt = _opt(gpu_decoder, S.KITTI_OPTIM, "KITTI", iters=2)
+    objs = [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in (S.kitti_object(i) for i in range(2))]
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
+    monkeypatch.setenv("DSR_LITE_VARIANT", "16")       # not a kernel of the shipped build
+    keep = []
+    ins = (L.ObjectIn * 2)()
+    for i, ob in enumerate(objs):
+        ins[i] = opt._object_in(*ob[:4], None, keep)
+    ctx = opt._ctx
+    h = C.c_void_p()
+    ctx.check(ctx.lib.dsr_batch_create(ctx.handle, opt.decoder.handle, C.byref(opt.params), 2, ins,
+                                       C.byref(h)), "create")
+    try:
+        ctx.check(ctx.lib.dsr_batch_run(h), "run")
+        ctx.check(ctx.lib.dsr_batch_sync(h), "sync")
+        monkeypatch.setenv("DSR_FWD_VARIANT", "0")     # after the run: must not be reported
+        monkeypatch.setenv("DSR_JAC_VARIANT", "0")
+        monkeypatch.setenv("DSR_SPLIT_RING", "3")
+        st = L.Stats()
+        ctx.check(ctx.lib.dsr_batch_stats(h, C.byref(st)), "stats")
+    finally:
+        ctx.lib.dsr_batch_destroy(h)
+    assert (st.lite_variant, st.fwd_variant, st.jac_variant, st.split_ring) == (1496, 12, 12, 2)
+    assert st.n_groups == 2 and st.prescan == 0

@@ -329,14 +329,33 @@ def test_keyframe_slot_capacity_is_bounded(monkeypatch):
     many_small = opt._slot_for(kf(8, 256, 300))        # 8 x 384 rays padded
     assert (many_small.max_obj, many_small.max_rays) == (8, 384)
     # one large object: growing the 8-object slot to 8 x 4096 rays would be 8x its need -> a new
-    # slot sized for it replaces the free one
+    # slot sized for it, BESIDE the free one (a keyframe that cannot grow a free slot
+    # within the bounds no longer destroys it and its captured graph)
     big = opt._slot_for(kf(1, 2048, 4000))
-    assert (big.max_obj, big.max_rays) == (1, 4096) and many_small.closed
+    assert (big.max_obj, big.max_rays) == (1, 4096) and not many_small.closed
     # a small keyframe inside the large slot's bound is served by it
     assert opt._slot_for(kf(1, 100, 1500)) is big
     # a keyframe far smaller than every free slot does not use them: a slot of its own
     tiny = opt._slot_for(kf(1, 64, 100))
     assert tiny is not big and (tiny.max_obj, tiny.max_rays) == (1, 128)
+    assert not big.closed and not many_small.closed and len(opt._slots) == 3
+    # the 8-object keyframe shape comes back: its slot (and graph) is still there
+    assert opt._slot_for(kf(8, 200, 300)) is many_small
+    # a fourth slot (the others in flight, so none can grow)
+    for sl in opt._slots:
+        sl.busy = True
+    fourth = opt._slot_for(kf(2, 1024, 1024))
+    for sl in opt._slots:
+        sl.busy = False
+    assert len(opt._slots) == 4 and not any(sl.closed for sl in (many_small, big, tiny, fourth))
+    assert opt._slot_for(kf(1, 100, 1500)) is big
+    # MAX_SLOTS reached and no free slot can serve or grow: the least recently used free slot
+    # (many_small; tiny is in flight) makes room, the others stay
+    tiny.busy = True
+    fifth = opt._slot_for(kf(1, 64, 60))
+    assert many_small.closed and not any(sl.closed for sl in (big, tiny, fourth))
+    assert len(opt._slots) == 4 and fifth in opt._slots and (fifth.max_obj, fifth.max_rays) == (1, 128)
+    tiny.busy = False
     # beyond SLOT_MAX_SAMPLES ray samples: one-shot
     monkeypatch.setattr(O.Optimizer, "SLOT_MAX_SAMPLES", 1 << 16)
     for sl in opt._slots:

@@ -23,6 +23,10 @@ if sys.argv[1] == "--compare":
 import synthetic as S  # noqa: E402
 from deep_sdf.workspace import decoder_from_state  # noqa: E402
 from reconstruct import _libdsr as L  # noqa: E402
+
+# an A/B against an older build (ABI 10: this script uses only entry points and record layouts
+# both ABIs share) — accept the library's own ABI number
+L.ABI_VERSION = C.CDLL(L.lib_path()).dsr_abi_version()
 from reconstruct.optimizer import sdf_eval  # noqa: E402
 import bench  # noqa: E402
 
