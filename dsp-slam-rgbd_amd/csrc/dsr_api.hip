@@ -3,6 +3,8 @@
 //
 // Build (gfx950 only, in-tree):  make -C dsp-slam-rgbd_amd/csrc   -> libdsr.so
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1937,52 +1939,199 @@ int dsr_batch_lite_diag(dsr_batch* b, int* rec, int n) {
   return 0;
 }
 
-// Multi-GPU from one process: longest-processing-time-first partition of
-// the objects over the devices (cost = n_rays * M + n_pts, the decoder work of one
-// iteration, greedy to the least loaded device; the same rule as reconstruct/parallel.py),
-// one host thread per device running its shard through dsr_reconstruct_batch, every
-// out-record written back in input order — host memory is the gather point, so no
-// collective is needed inside one process.  Objects never interact: each result is
-// bitwise the one a single-device batch gives.
-int dsr_reconstruct_multi(dsr_ctx* const* ctxs, const dsr_decoder* const* decs, int n_dev,
-                          const dsr_optim_params* p, int n_obj, const dsr_object_in* in, dsr_object_out* out) {
+// Multi-GPU from one process, replacing the per-detection loop of
+// LocalMapping_util.cc:165-206: longest-processing-time-first partition of the objects over the
+// devices (cost = n_rays * M + n_pts, the decoder work of one iteration, greedy to the least loaded
+// device, ties to the lower device; the rule of reconstruct/parallel.py), one host thread per
+// device runs its shard's batch, and ONE RCCL gather (ncclCommInitAll over the devices, ncclGather
+// to device 0 over xGMI) brings every shard's fixed-size dsr_object_out records to device 0, whose
+// single download is unpacked into input order.  Each shard's records sit in a slot of
+// max-shard-size records (the gather's equal counts): object i lands at record
+// dev[i] * maxn + slot[i] of the gathered buffer (dsr_gather_layout).  RCCL is loaded at run time;
+// when it is missing or its communicator cannot be built (e.g. two contexts on one device), the
+// records are gathered through host memory instead, and *path says which route ran.
+extern "C" int dsr_gather_layout(int n_obj, const dsr_object_in* in, int num_depth_samples, int n_dev, int* dev,
+                                 int* slot, int* maxn) {
+  if (n_obj <= 0 || !in || n_dev <= 0 || !dev || !slot || !maxn) return -2;
+  std::vector<int> order(n_obj);
+  for (int i = 0; i < n_obj; ++i) order[i] = i;
+  auto cost = [&](int i) { return (double)in[i].n_rays * num_depth_samples + in[i].n_pts; };
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
+  std::vector<double> load(n_dev, 0.0);
+  for (int i : order) {
+    const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    dev[i] = g;
+    load[g] += cost(i);
+  }
+  std::vector<int> cnt(n_dev, 0);
+  for (int i = 0; i < n_obj; ++i) slot[i] = cnt[dev[i]]++;   // input order within a shard
+  *maxn = *std::max_element(cnt.begin(), cnt.end());
+  return 0;
+}
+
+namespace {
+// RCCL entry points, resolved from librccl at first use (no link-time dependency: a host
+// without RCCL still loads libdsr and gathers through host memory)
+struct Rccl {
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclGather) gather = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    r.init_all = (decltype(r.init_all))dlsym(h, "ncclCommInitAll");
+    r.gather = (decltype(r.gather))dlsym(h, "ncclGather");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+    r.ok = r.init_all && r.gather && r.group_start && r.group_end && r.err;
+  });
+  return r;
+}
+// one communicator set per device list, built once and kept for the process (ncclCommInitAll
+// costs far more than a gather); an empty entry records a list RCCL refused
+std::mutex comm_mu;
+std::map<std::vector<int>, std::vector<ncclComm_t>> comm_cache;
+const std::vector<ncclComm_t>* comms_for(const std::vector<int>& devs, std::string& why) {
+  const Rccl& R = rccl();
+  if (!R.ok) {
+    why = "librccl not loadable";
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(comm_mu);
+  auto it = comm_cache.find(devs);
+  if (it == comm_cache.end()) {
+    std::vector<ncclComm_t> c(devs.size(), nullptr);
+    const ncclResult_t rc = R.init_all(c.data(), (int)devs.size(), devs.data());
+    if (rc != ncclSuccess) {
+      why = std::string("ncclCommInitAll: ") + R.err(rc);
+      c.clear();
+    }
+    it = comm_cache.emplace(devs, c).first;
+  }
+  if (it->second.empty()) {
+    if (why.empty()) why = "ncclCommInitAll refused this device list";
+    return nullptr;
+  }
+  return &it->second;
+}
+}  // namespace
+
+extern "C" int dsr_reconstruct_multi_ex(dsr_ctx* const* ctxs, const dsr_decoder* const* decs, int n_dev,
+                                        const dsr_optim_params* p, int n_obj, const dsr_object_in* in,
+                                        dsr_object_out* out, int* path) {
   if (!ctxs || !decs || n_dev <= 0 || !ctxs[0]) return -2;
   dsr_ctx* c0 = ctxs[0];
   if (!p || !out || (n_obj > 0 && !in)) return fail(c0, "null argument");
   if (n_obj <= 0) return fail(c0, "n_obj must be > 0");
   for (int g = 0; g < n_dev; ++g)
     if (!ctxs[g] || !decs[g]) return fail(c0, "null context or decoder");
-  std::vector<int> order(n_obj);
-  for (int i = 0; i < n_obj; ++i) order[i] = i;
-  auto cost = [&](int i) { return (double)in[i].n_rays * p->num_depth_samples + in[i].n_pts; };
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
-  std::vector<double> load(n_dev, 0.0);
+  if (path) *path = DSR_GATHER_HOST;
+  std::vector<int> dev(n_obj), slot(n_obj);
+  int maxn = 0;
+  dsr_gather_layout(n_obj, in, p->num_depth_samples, n_dev, dev.data(), slot.data(), &maxn);
   std::vector<std::vector<int>> shard(n_dev);
-  for (int i : order) {
-    const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    shard[g].push_back(i);
-    load[g] += cost(i);
-  }
+  for (int i = 0; i < n_obj; ++i) shard[dev[i]].push_back(i);
+  // the communicators first (one per device, device 0 the root), before any work is queued
+  std::vector<int> devs(n_dev);
+  for (int g = 0; g < n_dev; ++g) devs[g] = ctxs[g]->device;
+  std::string why;
+  const std::vector<ncclComm_t>* comms = comms_for(devs, why);
+  const size_t rec = sizeof(dsr_object_out);
+  std::vector<dsr_batch*> batch(n_dev, nullptr);
+  std::vector<void*> send(n_dev, nullptr);
+  void* recv = nullptr;
   std::vector<int> rc(n_dev, 0);
-  std::vector<std::vector<dsr_object_out>> res(n_dev);
   auto run = [&](int g) {
-    std::vector<int>& sh = shard[g];
+    dsr_ctx* ctx = ctxs[g];
+    hipSetDevice(ctx->device);
+    const std::vector<int>& sh = shard[g];
+    if (comms) {                                 // the shard's slot of the gather (zero-padded)
+      if (hipMalloc(&send[g], rec * (size_t)std::max(1, maxn)) != hipSuccess ||
+          hipMemsetAsync(send[g], 0, rec * (size_t)std::max(1, maxn), ctx->stream) != hipSuccess) {
+        rc[g] = fail(ctx, "hipMalloc failed (gather slot)");
+        return;
+      }
+    }
     if (sh.empty()) return;
-    std::sort(sh.begin(), sh.end());
     std::vector<dsr_object_in> sin;
     for (int i : sh) sin.push_back(in[i]);
-    res[g].resize(sh.size());
-    rc[g] = dsr_reconstruct_batch(ctxs[g], decs[g], p, (int)sh.size(), sin.data(), res[g].data(), nullptr);
+    if ((rc[g] = batch_create_impl(ctx, decs[g], p, (int)sh.size(), sin.data(), false, &batch[g])) != 0) return;
+    if ((rc[g] = dsr_batch_run(batch[g])) != 0) return;
+    if ((rc[g] = batch_finish(batch[g])) != 0) return;       // (its spare iteration included)
+    if (comms) {
+      if (hipMemcpyAsync(send[g], batch[g]->out, rec * sh.size(), hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+        rc[g] = fail(ctx, "hipMemcpyAsync failed (gather slot)");
+    } else {                                     // host gather: each shard downloads its own records
+      std::vector<dsr_object_out> res(sh.size());
+      if ((rc[g] = dsr_batch_download(batch[g], res.data())) != 0) return;
+      for (size_t k = 0; k < sh.size(); ++k) out[sh[k]] = res[k];
+    }
   };
-  std::vector<std::thread> th;
-  for (int g = 1; g < n_dev; ++g) th.emplace_back(run, g);
-  run(0);
-  for (auto& t : th) t.join();
-  for (int g = 0; g < n_dev; ++g)
-    if (rc[g]) return fail(c0, "device shard " + std::to_string(g) + ": " + ctxs[g]->err);
-  for (int g = 0; g < n_dev; ++g)
-    for (size_t k = 0; k < shard[g].size(); ++k) out[shard[g][k]] = res[g][k];
-  return 0;
+  if (comms) {
+    hipSetDevice(c0->device);
+    if (hipMalloc(&recv, rec * (size_t)maxn * n_dev) != hipSuccess) return fail(c0, "hipMalloc failed (gather)");
+  }
+  {
+    std::vector<std::thread> th;
+    for (int g = 1; g < n_dev; ++g) th.emplace_back(run, g);
+    run(0);
+    for (auto& t : th) t.join();
+  }
+  int status = 0;
+  for (int g = 0; g < n_dev && !status; ++g)
+    if (rc[g]) status = fail(c0, "device shard " + std::to_string(g) + ": " + ctxs[g]->err);
+  if (!status && comms) {
+    // ONE gather of every shard's slot to device 0 (ncclUint8 counts: the records are opaque)
+    const Rccl& R = rccl();
+    ncclResult_t nr = R.group_start();
+    for (int g = 0; g < n_dev && nr == ncclSuccess; ++g) {
+      hipSetDevice(ctxs[g]->device);
+      nr = R.gather(send[g], g == 0 ? recv : nullptr, rec * (size_t)maxn, ncclUint8, 0, (*comms)[g], ctxs[g]->stream);
+    }
+    const ncclResult_t ne = R.group_end();
+    if (nr == ncclSuccess) nr = ne;
+    if (nr != ncclSuccess) {
+      status = fail(c0, std::string("ncclGather: ") + R.err(nr));
+    } else {
+      std::vector<unsigned char> h(rec * (size_t)maxn * n_dev);
+      hipSetDevice(c0->device);
+      if (hipMemcpyAsync(h.data(), recv, h.size(), hipMemcpyDeviceToHost, c0->stream) != hipSuccess ||
+          hipStreamSynchronize(c0->stream) != hipSuccess) {
+        status = fail(c0, "gather download failed");
+      } else {
+        for (int i = 0; i < n_obj; ++i)
+          std::memcpy(&out[i], h.data() + rec * ((size_t)dev[i] * maxn + slot[i]), rec);
+        if (path) *path = DSR_GATHER_RCCL;
+      }
+    }
+  }
+  for (int g = 0; g < n_dev; ++g) {
+    hipSetDevice(ctxs[g]->device);
+    if (send[g]) {
+      hipStreamSynchronize(ctxs[g]->stream);
+      hipFree(send[g]);
+    }
+    if (batch[g]) dsr_batch_destroy(batch[g]);
+  }
+  if (recv) {
+    hipSetDevice(c0->device);
+    hipFree(recv);
+  }
+  return status;
+}
+
+int dsr_reconstruct_multi(dsr_ctx* const* ctxs, const dsr_decoder* const* decs, int n_dev,
+                          const dsr_optim_params* p, int n_obj, const dsr_object_in* in, dsr_object_out* out) {
+  return dsr_reconstruct_multi_ex(ctxs, decs, n_dev, p, n_obj, in, out, nullptr);
 }
 
 int dsr_reconstruct_batch(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_optim_params* p, int n_obj,

@@ -1946,140 +1946,359 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
 #ifdef DSR_SOLVE_PROFILE
   const long long tp1 = wall_clock64();
 #endif
-  // ---- LU with partial pivoting (torch.inverse, optimizer.py:188): 2 barriers per pivot.
-  // Pivot search of column k: first max |A[r][k]|, r >= k (LAPACK getrf), by wave 0, fused
-  // into the previous step's update of column k.  Per step: (X) row swap + column scale,
-  // (Y) rank-1 update; the arithmetic is getf2's (multiplier by reciprocal, one fma per
-  // element), so the factors are bitwise those of the 4-phase schedule.
-  // One 64-bit key per candidate: |v| bits (order-preserving for |v| >= 0) over 0xffff - row
-  // (ties: the first row); NaN rows key 0, never chosen (fabsf(NaN) > best is false).  The
-  // wave max (DPP reduction) is the first max; its signed value is read back from A, which
-  // wave 0 wrote before (LDS keeps a wave's accesses in order).
-  auto pivot_search = [&](int k, int r0, float v0, int r1, float v1) {   // wave 0, lanes' candidates
-    auto key = [](float v, int r) -> unsigned long long {
-      const float a = fabsf(v);
-      return (r < NPAR && a >= 0.f) ? ((unsigned long long)__float_as_uint(a) << 32) | (unsigned)(0xffff - r) : 0ull;
-    };
-    const unsigned long long k0 = key(v0, r0), k1 = key(v1, r1);
-    const unsigned long long km = __ockl_wfred_max_u64(k0 > k1 ? k0 : k1);
-    if (tid == 0) {
-      const int bi = km ? 0xffff - (int)(km & 0xffffffffull) : NPAR;
-      piv[k] = bi;
-      pivv[k] = bi < NPAR ? A[bi][k] : 0.f;
-    }
-  };
-  if (tid < 64) pivot_search(0, tid, A[tid][0], tid + 64, tid + 64 < NPAR ? A[tid + 64][0] : 0.f);
+  // ---- dx = inverse(H) b (optimizer.py:188: torch.inverse(H) then a mat-vec).  H is symmetric
+  // positive definite — J^T J / N terms, + I on the pose block, + k3 I on the code block,
+  // + s_damp on the scale, + k4 J_rot^T J_rot — so it is solved by a Cholesky factorisation
+  // H = L L^T in fp64, with b carried as an extra row of L (row NPAR: the forward substitution
+  // L y = b rides along in the factorisation) and one back substitution L^T dx = y: no pivot
+  // search, no row swaps, one barrier per column (the LU + explicit inverse
+  // it replaces took 63 + 21 us per solve).  dx is at least as accurate as the reference's fp32
+  // inverse-times-b (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_
+  // the_reference holds it against fp64 truth).  A non-positive or NaN pivot (an H with NaN or
+  // inf entries) falls back to the fp32 LU with partial pivoting below, the reference's own
+  // getrf / getri arithmetic, so those cases behave exactly as before.
+#ifndef DSR_CHOL_VARIANT
+#define DSR_CHOL_VARIANT 4
+#endif
+  constexpr int LP = NPAR + 3;                  // fp64 pitch 74: 16-byte aligned rows (the panel reads)
+  __shared__ __attribute__((aligned(16))) double Lc[NPAR + 1][LP];
+  __shared__ double rdg[NPAR];                  // 1 / L[c][c]
+  __shared__ int chol_bad;
+  for (int e = tid; e < (NPAR + 1) * NPAR; e += SOLVE_THREADS) {
+    const int a = e / NPAR, b = e - (e / NPAR) * NPAR;
+    if (b <= a) Lc[a][b] = (double)(a < NPAR ? A[a][b] : bv[b]);
+  }
+  if (tid == 0) chol_bad = 0;
   __syncthreads();
-  for (int k = 0; k < NPAR; ++k) {
-    const int p = piv[k];
-    {   // (X) swap rows k, p (every column but k); column k: pivot to the diagonal, scale below
-      const float pv = pivv[k];                            // = A[p][k] (written below)
-      const float rc = 1.0f / pv;
-      for (int c = tid; c < NPAR; c += SOLVE_THREADS)
-        if (c != k && p != k) { const float t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
-      for (int r = k + 1 + tid; r < NPAR; r += SOLVE_THREADS) {
-        const float x = (r == p) ? A[k][k] : A[r][k];      // post-swap row r's column-k value
-        A[r][k] = x * rc;
-        if (r == p) A[k][k] = pv;
+  // a double of lane 0 / lane k as a wave-uniform value (two v_readlane: no LDS round trip)
+  auto bcast0 = [](double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll)), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  };
+  auto bcastk = [](double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  };
+  // column c of L from its updated values v (wave 0; lane l holds rows c + l and c + 64 + l):
+  // 1/sqrt(d) from v_rsq_f64 and two Newton steps (full fp64 precision), no sqrt / divide chain
+  auto chol_col = [&](int c, double v0, double v1) {
+    const int r0 = c + tid, r1 = r0 + 64;
+#if DSR_CHOL_VARIANT & 1
+    const double d2 = __shfl(v0, 0);
+    if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
+    const double dd = sqrt(d2);
+    if (r0 == c) {
+      Lc[c][c] = dd;
+      rdg[c] = 1.0 / dd;
+    }
+    else if (r0 <= NPAR) Lc[r0][c] = v0 / dd;
+    if (r1 <= NPAR) Lc[r1][c] = v1 / dd;
+#else
+    const double d2 = bcast0(v0);
+    if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
+    double rs = __builtin_amdgcn_rsq(d2);
+    rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
+    rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
+    if (r0 == c) {
+      Lc[c][c] = d2 * rs;
+      rdg[c] = rs;
+    }
+    else if (r0 <= NPAR) Lc[r0][c] = v0 * rs;
+    if (r1 <= NPAR) Lc[r1][c] = v1 * rs;
+#endif
+  };
+#if DSR_CHOL_VARIANT >= 4
+  // Blocked right-looking Cholesky, panels of CPW columns: wave 0 factors a panel in registers
+  // (lane l holds rows c0 + l and c0 + 64 + l; the pivot value and the panel's L[c'][c] reach the
+  // other lanes by v_readlane), then all waves apply the panel to the trailing triangle (rows and
+  // columns >= c1, the b row included) — 2 barriers per panel instead of 1 per column.
+  constexpr int CPW = 8;
+  for (int c0 = 0; c0 < NPAR; c0 += CPW) {
+    const int c1 = min(c0 + CPW, NPAR);
+    if (tid < 64) {
+      const int r0 = c0 + tid, r1 = r0 + 64;
+      double a0[CPW], a1[CPW];
+#pragma unroll
+      for (int u = 0; u < CPW; ++u) {
+        const int c = c0 + u;
+        a0[u] = (c < c1 && r0 <= NPAR && c <= r0) ? Lc[r0][c] : 0.0;
+        a1[u] = (c < c1 && r1 <= NPAR) ? Lc[r1][c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < CPW; ++u) {
+        if (c0 + u < c1) {
+          const double d2 = bcastk(a0[u], u);                 // row c0 + u sits in lane u
+          if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
+          double rs = __builtin_amdgcn_rsq(d2);
+          rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
+          rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
+          a0[u] = (tid == u) ? d2 * rs : a0[u] * rs;
+          a1[u] = a1[u] * rs;
+          if (tid == u) rdg[c0 + u] = rs;
+#pragma unroll
+          for (int w = u + 1; w < CPW; ++w) {                   // the panel's later columns
+            if (c0 + w < c1) {
+              const double lwu = bcastk(a0[u], w);              // L[c0 + w][c0 + u]
+              a0[w] -= a0[u] * lwu;
+              a1[w] -= a1[u] * lwu;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < CPW; ++u) {
+        const int c = c0 + u;
+        if (c < c1 && r0 <= NPAR && c <= r0) Lc[r0][c] = a0[u];
+        if (c < c1 && r1 <= NPAR) Lc[r1][c] = a1[u];
       }
     }
     __syncthreads();
-    {   // (Y) trailing update; wave 0 owns column k+1 and searches its pivot
-      const int m = NPAR - k - 1;
-      if (tid < 64) {
-        if (k + 1 < NPAR) {
-          const int c = k + 1;
-          const int r0 = k + 1 + tid, r1 = r0 + 64;
-          float v0 = 0.f, v1 = 0.f;
-          if (r0 < NPAR) { v0 = __builtin_fmaf(-A[r0][k], A[k][c], A[r0][c]); A[r0][c] = v0; }
-          if (r1 < NPAR) { v1 = __builtin_fmaf(-A[r1][k], A[k][c], A[r1][c]); A[r1][c] = v1; }
-          pivot_search(k + 1, r0, v0, r1, v1);
+    // trailing update by the panel: A[i][j] -= sum_u L[i][c0+u] L[j][c0+u], c1 <= j <= i, j < NPAR,
+    // in 4 x 4 element blocks (block row bi >= block column bj), one per thread: the 8 panel values
+    // of its 4 rows and 4 columns are loaded once (16-byte reads) and reused across the block
+    {
+      const int nr = NPAR + 1 - c1, nb = (nr + 3) >> 2;
+      const int t = tid;
+      if (t < nb * (nb + 1) / 2) {
+        int bi = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
+        while (bi * (bi + 1) / 2 > t) --bi;
+        while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+        const int bj = t - bi * (bi + 1) / 2;
+        const int i0 = c1 + 4 * bi, j0 = c1 + 4 * bj;
+        double li[4][CPW], lj[4][CPW];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int i = min(i0 + m, NPAR), j = min(j0 + m, NPAR);
+#pragma unroll
+          for (int u = 0; u < CPW; u += 2) {
+            const double2 vi = *reinterpret_cast<const double2*>(&Lc[i][c0 + u]);
+            const double2 vj = *reinterpret_cast<const double2*>(&Lc[j][c0 + u]);
+            li[m][u] = vi.x; li[m][u + 1] = vi.y;
+            lj[m][u] = vj.x; lj[m][u + 1] = vj.y;
+          }
         }
-      } else if (m > 1) {         // rows k+1.., columns k+2..: a fixed 16 x 16 thread grid
-        static_assert(SOLVE_THREADS - 64 == 256, "trailing-update grid");
-        const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15;
-        for (int r = k + 1 + rr; r < NPAR; r += 16) {
-          const float ark = A[r][k];
-          for (int c = k + 2 + cc; c < NPAR; c += 16) A[r][c] = __builtin_fmaf(-ark, A[k][c], A[r][c]);
-        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + m, j = j0 + q;
+            if (i <= NPAR && j < NPAR && j <= i) {
+              double acc = Lc[i][j];
+#pragma unroll
+              for (int u = 0; u < CPW; ++u)
+                if (c0 + u < c1) acc -= li[m][u] * lj[q][u];
+              Lc[i][j] = acc;
+            }
+          }
       }
     }
     __syncthreads();
   }
+#else
+  if (tid < 64) chol_col(0, Lc[tid][0], 64 + tid <= NPAR ? Lc[64 + tid][0] : 0.0);
+  __syncthreads();
+  for (int k = 0; k + 1 < NPAR; ++k) {
+    if (tid < 64) {            // column k+1: its update by column k, then its scaling (look-ahead)
+      const int c = k + 1, r0 = c + tid, r1 = r0 + 64;
+      const double lck = Lc[c][k];
+      const double v0 = r0 <= NPAR ? Lc[r0][c] - Lc[r0][k] * lck : 0.0;
+      const double v1 = r1 <= NPAR ? Lc[r1][c] - Lc[r1][k] * lck : 0.0;
+      chol_col(c, v0, v1);
+    } else {                   // the rest of the trailing update: columns k+2.., rows j.. NPAR
+#if DSR_CHOL_VARIANT & 2
+      const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15;
+      for (int i = k + 2 + rr; i <= NPAR; i += 16) {
+        const double lik = Lc[i][k];
+        for (int j = k + 2 + cc; j <= i && j < NPAR; j += 16) Lc[i][j] -= lik * Lc[j][k];
+      }
+#else
+      // thread (rr, cc) of a 16 x 16 grid: rows k+2+rr+16m, columns k+2+cc+16q (m, q < 5); every
+      // operand is loaded before the first update so the LDS round trips overlap, and an element
+      // outside the triangle reads / writes the padding column LP-1 of row 0 instead of branching
+      const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15, b0 = k + 2;
+      constexpr int NB = (NPAR + 1 + 15) / 16;
+      double li[NB], lj[NB], a[NB][NB];
+      double* const pad = &Lc[0][LP - 1];
+#pragma unroll
+      for (int m = 0; m < NB; ++m) {
+        const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * m;
+        li[m] = *(i <= NPAR ? &Lc[i][k] : pad);
+        lj[m] = *(j < NPAR ? &Lc[j][k] : pad);
+      }
+#pragma unroll
+      for (int m = 0; m < NB; ++m)
+#pragma unroll
+        for (int q = 0; q <= m; ++q) {
+          const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * q;
+          a[m][q] = *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad);
+        }
+#pragma unroll
+      for (int m = 0; m < NB; ++m)
+#pragma unroll
+        for (int q = 0; q <= m; ++q) {
+          const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * q;
+          *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad) = a[m][q] - li[m] * lj[q];
+        }
+#endif
+    }
+    __syncthreads();
+  }
+#endif
 #ifdef DSR_SOLVE_PROFILE
   const long long tp2 = wall_clock64();
 #endif
-  // inverse(H) = U^-1 L^-1 P I in LDS: the row permutation of the identity, then the
-  // forward / back substitutions of getrs, one column per thread (each element
-  // accumulates in the column-solve order)
-  for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) X[e / NPAR][e % NPAR] = 0.f;
-  __syncthreads();
-  if (tid < 64) {
-    // P applied to the row indices of I: the pivots' swaps in order on a permutation held
-    // across wave 0 (lane i: perm[i] and perm[64 + i]) with lane reads / selects — a private
-    // array indexed by the run-time pivot would live in scratch memory, one dependent
-    // round trip per swap
-    static_assert(NPAR <= 128, "permutation held in two registers per lane");
-    const int lane = tid;
-    int pa = lane, pb = 64 + lane;
-    const int qa = piv[lane], qb = (64 + lane < NPAR) ? piv[64 + lane] : 0;
+  if (!chol_bad) {
+    if (tid < 64) {            // L^T dx = y (row NPAR of L), one dependent step per row, wave 0
+      const int r0 = tid, r1 = tid + 64;
+      double y0 = Lc[NPAR][r0], y1 = r1 < NPAR ? Lc[NPAR][r1] : 0.0;
+#pragma unroll
+      for (int kk = NPAR - 1; kk >= 0; --kk) {
+        const double yk = kk < 64 ? bcastk(y0, kk) : bcastk(y1, kk - 64);
+        const double xk = yk * rdg[kk];
+        if (r0 == kk) y0 = xk;
+        else if (r0 < kk) y0 -= Lc[kk][r0] * xk;
+        if (r1 == kk) y1 = xk;
+        else if (r1 < kk) y1 -= Lc[kk][r1] * xk;
+      }
+      dx[r0] = (float)y0;
+      if (r1 < NPAR) dx[r1] = (float)y1;
+    }
+    __syncthreads();
+  } else {
+    // ---- LU with partial pivoting (torch.inverse, optimizer.py:188): 2 barriers per pivot.
+    // Pivot search of column k: first max |A[r][k]|, r >= k (LAPACK getrf), by wave 0, fused
+    // into the previous step's update of column k.  Per step: (X) row swap + column scale,
+    // (Y) rank-1 update; the arithmetic is getf2's (multiplier by reciprocal, one fma per
+    // element), so the factors are bitwise those of the 4-phase schedule.
+    // One 64-bit key per candidate: |v| bits (order-preserving for |v| >= 0) over 0xffff - row
+    // (ties: the first row); NaN rows key 0, never chosen (fabsf(NaN) > best is false).  The
+    // wave max (DPP reduction) is the first max; its signed value is read back from A, which
+    // wave 0 wrote before (LDS keeps a wave's accesses in order).
+    auto pivot_search = [&](int k, int r0, float v0, int r1, float v1) {   // wave 0, lanes' candidates
+      auto key = [](float v, int r) -> unsigned long long {
+        const float a = fabsf(v);
+        return (r < NPAR && a >= 0.f) ? ((unsigned long long)__float_as_uint(a) << 32) | (unsigned)(0xffff - r) : 0ull;
+      };
+      const unsigned long long k0 = key(v0, r0), k1 = key(v1, r1);
+      const unsigned long long km = __ockl_wfred_max_u64(k0 > k1 ? k0 : k1);
+      if (tid == 0) {
+        const int bi = km ? 0xffff - (int)(km & 0xffffffffull) : NPAR;
+        piv[k] = bi;
+        pivv[k] = bi < NPAR ? A[bi][k] : 0.f;
+      }
+    };
+    if (tid < 64) pivot_search(0, tid, A[tid][0], tid + 64, tid + 64 < NPAR ? A[tid + 64][0] : 0.f);
+    __syncthreads();
     for (int k = 0; k < NPAR; ++k) {
-      const int p = (k < 64) ? __builtin_amdgcn_readlane(qa, k) : __builtin_amdgcn_readlane(qb, k - 64);
-      if (p != k) {
-        const int vk = (k < 64) ? __builtin_amdgcn_readlane(pa, k) : __builtin_amdgcn_readlane(pb, k - 64);
-        const int vp = (p < 64) ? __builtin_amdgcn_readlane(pa, p) : __builtin_amdgcn_readlane(pb, p - 64);
-        if (k < 64) pa = (lane == k) ? vp : pa; else pb = (lane == k - 64) ? vp : pb;
-        if (p < 64) pa = (lane == p) ? vk : pa; else pb = (lane == p - 64) ? vk : pb;
+      const int p = piv[k];
+      {   // (X) swap rows k, p (every column but k); column k: pivot to the diagonal, scale below
+        const float pv = pivv[k];                            // = A[p][k] (written below)
+        const float rc = 1.0f / pv;
+        for (int c = tid; c < NPAR; c += SOLVE_THREADS)
+          if (c != k && p != k) { const float t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+        for (int r = k + 1 + tid; r < NPAR; r += SOLVE_THREADS) {
+          const float x = (r == p) ? A[k][k] : A[r][k];      // post-swap row r's column-k value
+          A[r][k] = x * rc;
+          if (r == p) A[k][k] = pv;
+        }
       }
+      __syncthreads();
+      {   // (Y) trailing update; wave 0 owns column k+1 and searches its pivot
+        const int m = NPAR - k - 1;
+        if (tid < 64) {
+          if (k + 1 < NPAR) {
+            const int c = k + 1;
+            const int r0 = k + 1 + tid, r1 = r0 + 64;
+            float v0 = 0.f, v1 = 0.f;
+            if (r0 < NPAR) { v0 = __builtin_fmaf(-A[r0][k], A[k][c], A[r0][c]); A[r0][c] = v0; }
+            if (r1 < NPAR) { v1 = __builtin_fmaf(-A[r1][k], A[k][c], A[r1][c]); A[r1][c] = v1; }
+            pivot_search(k + 1, r0, v0, r1, v1);
+          }
+        } else if (m > 1) {         // rows k+1.., columns k+2..: a fixed 16 x 16 thread grid
+          static_assert(SOLVE_THREADS - 64 == 256, "trailing-update grid");
+          const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15;
+          for (int r = k + 1 + rr; r < NPAR; r += 16) {
+            const float ark = A[r][k];
+            for (int c = k + 2 + cc; c < NPAR; c += 16) A[r][c] = __builtin_fmaf(-ark, A[k][c], A[r][c]);
+          }
+        }
+      }
+      __syncthreads();
     }
-    X[lane][pa] = 1.f;
-    if (64 + lane < NPAR) X[64 + lane][pb] = 1.f;
+    // inverse(H) = U^-1 L^-1 P I in LDS: the row permutation of the identity, then the
+    // forward / back substitutions of getrs, one column per thread (each element
+    // accumulates in the column-solve order)
+    for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS) X[e / NPAR][e % NPAR] = 0.f;
+    __syncthreads();
+    if (tid < 64) {
+      // P applied to the row indices of I: the pivots' swaps in order on a permutation held
+      // across wave 0 (lane i: perm[i] and perm[64 + i]) with lane reads / selects — a private
+      // array indexed by the run-time pivot would live in scratch memory, one dependent
+      // round trip per swap
+      static_assert(NPAR <= 128, "permutation held in two registers per lane");
+      const int lane = tid;
+      int pa = lane, pb = 64 + lane;
+      const int qa = piv[lane], qb = (64 + lane < NPAR) ? piv[64 + lane] : 0;
+      for (int k = 0; k < NPAR; ++k) {
+        const int p = (k < 64) ? __builtin_amdgcn_readlane(qa, k) : __builtin_amdgcn_readlane(qb, k - 64);
+        if (p != k) {
+          const int vk = (k < 64) ? __builtin_amdgcn_readlane(pa, k) : __builtin_amdgcn_readlane(pb, k - 64);
+          const int vp = (p < 64) ? __builtin_amdgcn_readlane(pa, p) : __builtin_amdgcn_readlane(pb, p - 64);
+          if (k < 64) pa = (lane == k) ? vp : pa; else pb = (lane == k - 64) ? vp : pb;
+          if (p < 64) pa = (lane == p) ? vk : pa; else pb = (lane == p - 64) ? vk : pb;
+        }
+      }
+      X[lane][pa] = 1.f;
+      if (64 + lane < NPAR) X[64 + lane][pb] = 1.f;
+    }
+    __syncthreads();
+    // Column c is solved by the 4 lanes 4c..4c+3 of one wave, lane `sub` holding rows
+    // i = sub + 4m (m < 18) in registers; a pivot row's value reaches the quad by a DPP
+    // broadcast, A is read as LDS broadcasts.  No barriers; each element is updated by one
+    // lane in the column-solve order (bitwise the getrs substitutions).
+    if (tid < 4 * NPAR) {
+      const int c = tid >> 2, sub = tid & 3;
+      constexpr int NM = (NPAR + 3) / 4;
+      float x[NM];
+  #pragma unroll
+      for (int m = 0; m < NM; ++m) x[m] = (sub + 4 * m < NPAR) ? X[sub + 4 * m][c] : 0.f;
+  #pragma unroll
+      for (int l = 0; l < NPAR - 1; ++l) {   // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
+        const float xl = quad_bcast(x[l >> 2], l & 3);
+  #pragma unroll
+        for (int m = l / 4; m < NM; ++m) {
+          const int i = sub + 4 * m;
+          if (i > l && i < NPAR) x[m] = __builtin_fmaf(-A[i][l], xl, x[m]);
+        }
+      }
+  #pragma unroll
+      for (int i = NPAR - 1; i >= 0; --i) {  // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
+        const float xi = quad_bcast(x[i >> 2], i & 3) / A[i][i];
+        if (sub == (i & 3)) x[i >> 2] = xi;
+  #pragma unroll
+        for (int m = 0; 4 * m < i; ++m) {
+          const int r = sub + 4 * m;
+          if (r < i) x[m] = __builtin_fmaf(-A[r][i], xi, x[m]);
+        }
+      }
+  #pragma unroll
+      for (int m = 0; m < NM; ++m)
+        if (sub + 4 * m < NPAR) X[sub + 4 * m][c] = x[m];
+    }
+    __syncthreads();
+    if (tid < NPAR) {                     // dx = inverse(H) b
+      float s = 0.f;
+      for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
+      dx[tid] = s;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  // Column c is solved by the 4 lanes 4c..4c+3 of one wave, lane `sub` holding rows
-  // i = sub + 4m (m < 18) in registers; a pivot row's value reaches the quad by a DPP
-  // broadcast, A is read as LDS broadcasts.  No barriers; each element is updated by one
-  // lane in the column-solve order (bitwise the getrs substitutions).
-  if (tid < 4 * NPAR) {
-    const int c = tid >> 2, sub = tid & 3;
-    constexpr int NM = (NPAR + 3) / 4;
-    float x[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) x[m] = (sub + 4 * m < NPAR) ? X[sub + 4 * m][c] : 0.f;
-#pragma unroll
-    for (int l = 0; l < NPAR - 1; ++l) {   // L (unit diagonal): X[i] -= A[i][l] X[l], i > l
-      const float xl = quad_bcast(x[l >> 2], l & 3);
-#pragma unroll
-      for (int m = l / 4; m < NM; ++m) {
-        const int i = sub + 4 * m;
-        if (i > l && i < NPAR) x[m] = __builtin_fmaf(-A[i][l], xl, x[m]);
-      }
-    }
-#pragma unroll
-    for (int i = NPAR - 1; i >= 0; --i) {  // U: X[i] /= A[i][i], then X[r] -= A[r][i] X[i], r < i
-      const float xi = quad_bcast(x[i >> 2], i & 3) / A[i][i];
-      if (sub == (i & 3)) x[i >> 2] = xi;
-#pragma unroll
-      for (int m = 0; 4 * m < i; ++m) {
-        const int r = sub + 4 * m;
-        if (r < i) x[m] = __builtin_fmaf(-A[r][i], xi, x[m]);
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-      if (sub + 4 * m < NPAR) X[sub + 4 * m][c] = x[m];
-  }
-  __syncthreads();
 #ifdef DSR_SOLVE_PROFILE                 // (tools: per-phase wall clock of block 0, 100 MHz ticks)
   const long long tp3 = wall_clock64();
   if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2);
 #endif
-  if (tid < NPAR) {                     // dx = inverse(H) b
-    float s = 0.f;
-    for (int l = 0; l < NPAR; ++l) s = __builtin_fmaf(X[tid][l], bv[l], s);
-    dx[tid] = s;
-  }
-  __syncthreads();
   if (tid < CODE) zbuf[o * CODE + tid] = z[tid] + P.lr * dx[NPOSE + tid];   // :194
   if (tid == 0) {
     float xi[NPOSE], dT[16], Tn[16], Tprev[16];

@@ -71,6 +71,7 @@ class Trace(C.Structure):
 
 ABI_VERSION = 11         # include/dsr.h DSR_ABI_VERSION
 BATCH_GRAPH = 1          # include/dsr.h DSR_BATCH_GRAPH
+GATHER_HOST, GATHER_RCCL = 0, 1   # include/dsr.h DSR_GATHER_* (dsr_reconstruct_multi_ex)
 
 
 class Stats(C.Structure):
@@ -141,6 +142,10 @@ SIGNATURES = {
     "dsr_reconstruct_multi": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
                                         C.POINTER(OptimParams), C.c_int, C.POINTER(ObjectIn),
                                         C.POINTER(ObjectOut)]),
+    "dsr_reconstruct_multi_ex": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
+                                           C.POINTER(OptimParams), C.c_int, C.POINTER(ObjectIn),
+                                           C.POINTER(ObjectOut), IP]),
+    "dsr_gather_layout": (C.c_int, [C.c_int, C.POINTER(ObjectIn), C.c_int, C.c_int, IP, IP, IP]),
     "dsr_mesher_create": (C.c_int, [C.c_void_p, C.c_void_p, FP, C.c_int, C.POINTER(C.c_void_p)]),
     "dsr_mesher_run": (C.c_int, [C.c_void_p, FP, C.c_float, FP, C.c_int, IP, C.c_int, IP, IP]),
     "dsr_mesher_destroy": (C.c_int, [C.c_void_p]),

@@ -295,12 +295,14 @@ class Optimizer(object):
                                               ins, L.fptr(out)), "dsr_pose_only_batch")
         return [out[i] for i in range(n)]
 
-    def reconstruct_objects_multi(self, objects, decoders):
+    def reconstruct_objects_multi(self, objects, decoders, return_path=False):
         """``reconstruct_objects`` spread over several devices from ONE process
-        (dsr_reconstruct_multi): ``decoders`` holds one decoder handle per device (e.g.
+        (dsr_reconstruct_multi_ex): ``decoders`` holds one decoder handle per device (e.g.
         ``[decoder_from_state(state, specs, device=g) for g in range(n)]``); objects are
-        LPT-partitioned, each device's shard runs on its own host thread.  One process
-        per GPU over RCCL is reconstruct.parallel.reconstruct_sharded."""
+        LPT-partitioned, each device's shard runs on its own host thread and one RCCL gather
+        returns the records to the first device (host memory when RCCL refuses the device
+        list); ``return_path`` adds which ("rccl" / "host").  One process per GPU is
+        reconstruct.parallel.reconstruct_sharded."""
         n = len(objects)
         if n == 0:
             return []
@@ -313,12 +315,15 @@ class Optimizer(object):
         ctxs = (C.c_void_p * nd)(*[d.ctx.handle.value for d in decoders])
         decs = (C.c_void_p * nd)(*[d.handle.value for d in decoders])
         ctx = decoders[0].ctx
-        ctx.check(ctx.lib.dsr_reconstruct_multi(ctxs, decs, nd, C.byref(self.params), n, ins, outs),
-                  "dsr_reconstruct_multi")
+        path = C.c_int(-1)
+        ctx.check(ctx.lib.dsr_reconstruct_multi_ex(ctxs, decs, nd, C.byref(self.params), n, ins, outs,
+                                                   C.byref(path)), "dsr_reconstruct_multi_ex")
         res = [self._result(outs[i], self.code_len) for i in range(n)]
         for i in range(n):
             res[i]["iters_done"] = int(outs[i].iters_done)
             res[i]["fail_reason"] = L.FAIL_REASONS.get(int(outs[i].fail_reason), "?")
+        if return_path:
+            return res, ("rccl" if path.value == L.GATHER_RCCL else "host")
         return res
 
     def compute_sdf_loss_objectpoint_zhjd(self, pts_surface_obj, code):

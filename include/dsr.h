@@ -303,15 +303,28 @@ int dsr_mesher_destroy(dsr_mesher* m);
 int dsr_mc_volume(dsr_ctx* ctx, const float* vol, int vol_dim, float level, float* verts, int vcap,
                   int* faces, int fcap, int* n_verts, int* n_faces);
 
-/* ---- multi-GPU from one process (SURVEY.md §8e): replaces the per-detection loop
+/* ---- multi-GPU from one process (SURVEY.md §5 / §8e): replaces the per-detection loop
  * LocalMapping_util.cc:165-206 spread over devices.  ctx[g] / dec[g] are one context and
  * its decoder per device; objects are LPT-partitioned (cost n_rays*M + n_pts), each
- * device's shard runs on its own host thread through dsr_reconstruct_batch, and out[] is
- * filled in input order (results bitwise equal to a one-device batch).  One process per
- * GPU over RCCL is the Python route (reconstruct/parallel.py). */
+ * device's shard runs on its own host thread, and ONE RCCL gather (ncclCommInitAll over the
+ * devices, ncclGather of the fixed-size dsr_object_out records to ctx[0]'s device, ABI 11)
+ * returns them; out[] is filled in input order (results bitwise equal to a one-device batch).
+ * RCCL is loaded at run time; without it, or when it refuses the device list (two contexts
+ * on one device), the records are gathered through host memory: *path (may be NULL) reports
+ * DSR_GATHER_RCCL or DSR_GATHER_HOST.  One process per GPU is reconstruct/parallel.py. */
+#define DSR_GATHER_HOST 0
+#define DSR_GATHER_RCCL 1
+int dsr_reconstruct_multi_ex(dsr_ctx* const* ctx, const dsr_decoder* const* dec, int n_dev,
+                             const dsr_optim_params* p, int n_obj, const dsr_object_in* in,
+                             dsr_object_out* out, int* path);
 int dsr_reconstruct_multi(dsr_ctx* const* ctx, const dsr_decoder* const* dec, int n_dev,
                           const dsr_optim_params* p, int n_obj, const dsr_object_in* in,
-                          dsr_object_out* out);
+                          dsr_object_out* out);   /* = _ex with path NULL */
+/* Host-only (no device needed): the multi-device layout — dev[i] the device of object i (LPT),
+ * slot[i] its record within that device's shard, *maxn the largest shard (every device's gather
+ * slot holds maxn records; object i is record dev[i] * maxn + slot[i] of the gathered buffer). */
+int dsr_gather_layout(int n_obj, const dsr_object_in* in, int num_depth_samples, int n_dev, int* dev,
+                      int* slot, int* maxn);
 
 /* ---- pose-only SE(3) GN: replaces Optimizer.estimate_pose_cam_obj
  * (optimizer.py:46-87).  t_co_se3: 4x4 SE(3) camera<-object, scale: object scale,

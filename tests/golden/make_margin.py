@@ -58,8 +58,12 @@ iteration and lands within
 ``SPREAD_MAX`` (the contract itself) of the 1-thread result.  On inputs
 that pass both screens the build must reproduce the reference's final
 ``t_cam_obj``, ``code`` and ``loss`` (optimizer.py:202-205) to the north star's
-1e-3 / 1e-4.  Candidates use fewer rays than the bench object (fewer samples near
-a threshold); the measured margins and spreads of rejected candidates are stored
+1e-3 / 1e-4.  The third screen (round 6, ``--conditioning``) is the GN step's own
+conditioning at the fp32 level (tools/f8_conditioning.py): from every recorded state,
+perturbed by as much as the fp32 oracle's own state is off there, the fp64 oracle's next
+state must stay within the contract — otherwise no implementation that rounds
+differently from the reference can be held to the fixture's end point.  Candidates use
+fewer rays than the bench object (fewer samples near a threshold); the measured margins and spreads of rejected candidates are stored
 too (``f8_screen.npz``), including full-size 2048-point KITTI objects, to show
 what does not qualify and why.
 """
@@ -255,6 +259,22 @@ def ensemble_spread(ref, dec, cfg, data_type, ob, base, base_k=None, members=Non
     return spread
 
 
+_COND = None
+
+
+def conditioning_of(out):
+    """tools/f8_conditioning.py's record for a packed candidate (``out``: the fixture arrays)"""
+    global _COND
+    if _COND is None:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import f8_conditioning as FC
+
+        _COND = (FC, FC.decoders())
+    FC, (d64, d32) = _COND
+    return FC.conditioning(out, d64, d32)
+
+
 def screen(ref, dec, name, cfg, data_type, ob):
     jo = cfg["joint_optim"]
     t0 = time.time()
@@ -287,6 +307,10 @@ def main():
     ap.add_argument("--no-full", action="store_true", help="skip the full-size KITTI objects")
     ap.add_argument("--family", default="", help="only these families, e.g. redwood3it,kitti3it")
     ap.add_argument("--screen-file", default="f8_screen.npz")
+    ap.add_argument("--seed-base", type=int, default=-1, help="first seed (default 5000 / 6000)")
+    ap.add_argument("--tries", type=int, default=-1, help="candidates per family (default: the family's)")
+    ap.add_argument("--conditioning", action="store_true",
+                    help="also require a well-conditioned GN step at every iteration (round 6)")
     args = ap.parse_args()
     only = {int(x) for x in args.seeds.split(",") if x.strip()}
     import torch
@@ -303,6 +327,7 @@ def main():
     redwood = lambda s: S.make_object(s, n_pts=512, scale=1.0, tz=3.0, upright=False)  # noqa: E731
     kitti = lambda s: tilted(S.make_object(s, n_pts=2048, scale=2.0, tz=15.0, upright=True), s)  # noqa
     kitti512 = lambda s: tilted(S.make_object(s, n_pts=512, scale=2.0, tz=15.0, upright=True), s)  # noqa
+    redwood2048 = lambda s: S.make_object(s, n_pts=2048, scale=1.0, tz=3.0, upright=False)  # noqa: E731
     families = [
         # (tag, optim, data_type, object factory(seed), n_fg, n_bg, wanted, max tries)
         ("redwood", S.REDWOOD_OPTIM, "Redwood", redwood, 32, 8, 2, 400),
@@ -320,6 +345,14 @@ def main():
         ("kitti2it", iters(S.KITTI_OPTIM, 2), "KITTI", kitti, 32, 8, 3, 200),
         ("kitti2it_r64", iters(S.KITTI_OPTIM, 2), "KITTI", kitti, 64, 8, 2, 200),
         ("kitti2it_p512", iters(S.KITTI_OPTIM, 2), "KITTI", kitti512, 32, 8, 2, 200),
+        # round 6: the Redwood parameter set at its own 5 iterations
+        # (config_redwood_01053.json:26), screened with --conditioning.  Each hidden-ReLU kink
+        # flip of a Jacobian point moves H by ~1/N of that point's share (the sdf term is a mean
+        # over N surface points, the render term over K), so more surface points and fewer rays
+        # make each flip smaller: 2048 points, 16 + 4 rays
+        ("redwood5_p2048_r16", S.REDWOOD_OPTIM, "Redwood", redwood2048, 16, 4, 2, 400),
+        ("redwood5_p2048", S.REDWOOD_OPTIM, "Redwood", redwood2048, 32, 8, 2, 400),
+        ("redwood5_r16", S.REDWOOD_OPTIM, "Redwood", redwood, 16, 4, 2, 400),
     ]
     if args.family:
         families = [f for f in families if f[0] in args.family.split(",")]
@@ -328,8 +361,11 @@ def main():
     screened = []
     for tag, cfg, dtp, fac, n_fg, n_bg, want, tries in families:
         got = 0
+        if args.tries > 0:
+            tries = args.tries
         for k in range(tries):
-            seed = 5000 + k if tag.startswith("redwood") else 6000 + k
+            base = args.seed_base if args.seed_base >= 0 else (5000 if tag.startswith("redwood") else 6000)
+            seed = base + k
             if only and seed not in only:
                 continue
             ob = reduce_rays(fac(seed), n_fg, n_bg)
@@ -339,6 +375,17 @@ def main():
             if not (ok and consistent):
                 continue
             out = MG.pack_traj(r, its)
+            if args.conditioning:
+                out_c = dict(out, obj_t_cam_obj=ob.t_cam_obj, obj_pts=ob.pts, obj_rays=ob.rays, obj_depth=ob.depth,
+                             data_type=np.array(dtp), num_iterations=np.array(cfg["joint_optim"]["num_iterations"]))
+                c = conditioning_of(out_c)
+                mins["cond_worst"] = max(c["worst_next_state_deviation"], default=0.0)
+                print(f"    conditioning: worst next-state deviation "
+                      f"{' '.join(f'{w:.1e}' for w in c['worst_next_state_deviation'])}"
+                      f" -> {'ok' if c['well_conditioned'] else 'ILL-CONDITIONED'}", flush=True)
+                if not c["well_conditioned"]:
+                    screened[-1] = (name, False, consistent, mins)
+                    continue
             out.update({"obj_t_cam_obj": ob.t_cam_obj, "obj_pts": ob.pts, "obj_rays": ob.rays,
                         "obj_depth": ob.depth, "seed": np.array(seed), "data_type": np.array(dtp),
                         "n_fg": np.array(n_fg), "n_bg": np.array(n_bg),
@@ -364,11 +411,11 @@ def main():
                 mins["spread_pose"], mins["spread_code"], mins["spread_loss"] = (float(x) for x in sp)
             screened.append((f"kitti_full{i}", ok, consistent, mins))
     keys = ("band", "dedo", "ball", "ball_all", "rot_ulps", "clamp", "huber_render", "huber_sdf",
-            "spread_pose", "spread_code", "spread_loss")
+            "spread_pose", "spread_code", "spread_loss") + (("cond_worst",) if args.conditioning else ())
     np.savez_compressed(os.path.join(HERE, args.screen_file),
                         names=np.array([s[0] for s in screened]), ok=np.array([s[1] for s in screened]),
                         consistent=np.array([s[2] for s in screened]),
-                        margins=np.array([[s[3][k] for k in keys] for s in screened]),
+                        margins=np.array([[s[3].get(k, np.nan) for k in keys] for s in screened]),
                         margin_keys=np.array(keys), **meta)
 
 

@@ -128,3 +128,40 @@ def test_c_stress_no_device_paths(exe_name):
     p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "stress ok" in p.stdout
+
+
+def test_gather_layout_of_the_multi_device_entry_point():
+    """dsr_reconstruct_multi_ex gathers every device's shard of fixed-size
+    dsr_object_out records to device 0 in one ncclGather of equal slots: object i is record
+    dev[i] * maxn + slot[i].  dsr_gather_layout (host-only, no device) is that layout: the LPT
+    partition of reconstruct/parallel.py (cost n_rays * M + n_pts), input order within a shard,
+    every record position used once, maxn the largest shard."""
+    import ctypes
+
+    import numpy as np
+
+    from reconstruct import _libdsr as L
+    from reconstruct.parallel import lpt_partition
+
+    lib = L.load_library()
+    rng = np.random.default_rng(5)
+    for n_obj, n_dev in ((1, 1), (7, 2), (64, 8), (13, 8), (5, 8)):
+        ins = (L.ObjectIn * n_obj)()
+        costs = []
+        for i in range(n_obj):
+            ins[i].n_rays = int(rng.integers(0, 3000))
+            ins[i].n_pts = int(rng.integers(0, 4096))
+            costs.append(ins[i].n_rays * 50 + ins[i].n_pts)
+        dev = np.zeros(n_obj, np.int32)
+        slot = np.zeros(n_obj, np.int32)
+        maxn = ctypes.c_int(0)
+        assert lib.dsr_gather_layout(n_obj, ins, 50, n_dev, L.iptr(dev), L.iptr(slot), ctypes.byref(maxn)) == 0
+        shards = lpt_partition(costs, n_dev)
+        for g in range(n_dev):
+            mine = sorted(np.nonzero(dev == g)[0].tolist())
+            assert mine == sorted(shards[g]), (n_obj, n_dev, g)
+            assert slot[mine].tolist() == list(range(len(mine)))       # input order within the shard
+        assert maxn.value == max(len(s) for s in shards)
+        pos = dev.astype(np.int64) * maxn.value + slot
+        assert len(set(pos.tolist())) == n_obj and pos.max() < n_dev * maxn.value
+    assert ctypes.sizeof(L.ObjectOut) % 4 == 0                          # records gathered as bytes

@@ -69,13 +69,20 @@ def test_reconstruct_multi_equals_one_context(gpu_decoder, full_layers):
         o = S.make_object(700 + i, n_pts=150 + 61 * i, n_bg=20 + 9 * i, scale=1.0, tz=3.0, upright=False)
         objs.append((o.t_cam_obj, o.pts, o.rays, o.depth, None))
     one = opt.reconstruct_objects(objs)
-    multi = opt.reconstruct_objects_multi(objs, [gpu_decoder, dec2])
-    for a, b in zip(one, multi):
-        assert a["is_good"] == b["is_good"]
-        assert a["loss"] == b["loss"]
-        if a["is_good"]:
-            assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"])
-            assert np.array_equal(a["code"], b["code"])
+    # two contexts on ONE device: RCCL refuses a duplicate device, so the records come back
+    # through host memory (the fallback) — and say so
+    multi, path = opt.reconstruct_objects_multi(objs, [gpu_decoder, dec2], return_path=True)
+    assert path == "host"
+    # one device through RCCL: ncclCommInitAll over [0], one ncclGather
+    rccl1, path1 = opt.reconstruct_objects_multi(objs, [gpu_decoder], return_path=True)
+    assert path1 == "rccl"
+    for res in (multi, rccl1):
+        for a, b in zip(one, res):
+            assert a["is_good"] == b["is_good"]
+            assert a["loss"] == b["loss"]
+            if a["is_good"]:
+                assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"])
+                assert np.array_equal(a["code"], b["code"])
 
 
 def test_zero_iterations_returns_input(gpu_decoder):

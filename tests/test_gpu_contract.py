@@ -41,6 +41,11 @@ pytestmark = pytest.mark.gpu
 
 F8 = sorted(glob.glob(os.path.join(GOLDEN, "f8_margin_*.npz")))
 POSE_TOL, CODE_TOL, LOSS_TOL = 1e-3, 1e-3, 1e-4
+# an ill-conditioned fixture's end point (tests/golden/f8_conditioning.json) is still
+# held, to a looser bound pinned to a number: the split-fp16 kernels of round 5 landed redwood_s5359
+# at rotation 1.47e-2, code 0.225, loss 2.70e-2 from the reference's end point (r5al), the state
+# error its iteration-2 step amplifies 1e4-fold; the bounds are about twice that
+ILL_POSE_TOL, ILL_CODE_TOL, ILL_LOSS_TOL = 3e-2, 0.5, 6e-2
 
 
 def contract_errors(T, z, loss, f):
@@ -75,6 +80,17 @@ def _run(dec, f, optim, dtp):
 
 def test_fixtures_present():
     assert len(F8) >= 2, "margin-screened fixtures missing (python tests/golden/make_margin.py)"
+
+
+def test_well_conditioned_fixtures_at_the_full_iteration_count():
+    """at least two fixtures run the Redwood configuration's own 5 GN iterations
+    (config_redwood_01053.json:26) and are well-conditioned at every step, so
+    test_final_state_matches_reference holds their END POINT to the strict contract on both decode
+    paths (round 6 screen: tests/golden/make_margin.py --conditioning, 1,000 seeds)."""
+    full = [p for p in F8 if str(np.load(p)["data_type"]) == "Redwood"
+            and int(np.load(p)["n_iters_run"]) == S.REDWOOD_OPTIM["joint_optim"]["num_iterations"]
+            and _conditioning(p) is None]
+    assert len(full) >= 2, full
 
 
 def _conditioning(path):
@@ -130,10 +146,18 @@ def test_final_state_matches_reference(gpu_decoder, oracle_dec, path, lite, monk
         tro = _step_fp64_at(oracle_dec, f, optim, t["t_obj_cam"][e], t["z"][e])
         d = np.asarray(t["dx"][e], np.float64) - tro.dx
         es = float(np.sqrt(max(d @ tro.H @ d, 0.0) / max(tro.dx @ tro.H @ tro.dx, 1e-300)))
+        Tg, Tr = t["t_obj_cam"][e].astype(np.float64), f["it_t_obj_cam"][e].astype(np.float64)
+        drift = float(np.abs(Tg - Tr).max() / np.abs(Tr).max())
         print(f"it {e}: K gpu {int(t['k'][e])} reference {int(f['it_k'][e])}, fp64 oracle at the GPU's state "
-              f"{tro.k}; step vs the oracle's from the GPU's state {es:.1e} (H-norm)")
+              f"{tro.k}; step vs the oracle's from the GPU's state {es:.1e} (H-norm); state drift {drift:.1e}, "
+              f"band margin {float(f['margin_band'][e]):.1e}")
         assert int(tro.k) == int(t["k"][e]), (e, int(tro.k), int(t["k"][e]))
         assert abs(int(t["k"][e]) - int(f["it_k"][e])) <= 1 or ill is not None, (e, t["k"], f["it_k"])
+        if t["k"][e] != f["it_k"][e] and ill is None:
+            # a K that differs from the reference's is accepted only where the GPU's own
+            # state has drifted from the reference's by more than the fixture's band margin at that
+            # iteration (sdf and object coordinates share a unit; x2 for |grad sdf| > 1)
+            assert float(f["margin_band"][e]) < 2.0 * drift, (e, float(f["margin_band"][e]), drift)
         if ill is not None:
             assert es <= 1e-2, (e, es)
     for e in range(n_it):
@@ -147,6 +171,10 @@ def test_final_state_matches_reference(gpu_decoder, oracle_dec, path, lite, monk
         assert e_rot <= POSE_TOL and e_t <= POSE_TOL, (e_rot, e_t)
         assert e_z <= CODE_TOL, e_z
         assert e_l <= LOSS_TOL, e_l
+    else:
+        assert e_rot <= ILL_POSE_TOL and e_t <= ILL_POSE_TOL, (e_rot, e_t)
+        assert e_z <= ILL_CODE_TOL, e_z
+        assert e_l <= ILL_LOSS_TOL, e_l
 
 
 @pytest.mark.parametrize("path", F8, ids=[os.path.basename(p)[10:-4] for p in F8])

@@ -40,9 +40,10 @@ N_DIR, CONTRACT, FLOOR = 6, 1e-3, 1e-7
 
 
 def conditioning(path, d64, d32):
-    """{perturbation, worst_next_state_deviation, well_conditioned} of one F8 fixture"""
-    f = np.load(path, allow_pickle=False)
-    optim, _ = optim_of(f)
+    """{perturbation, worst_next_state_deviation, well_conditioned} of one F8 fixture (a path, or
+    the fixture's arrays as a mapping: tests/golden/make_margin.py screens candidates with it)"""
+    f = np.load(path, allow_pickle=False) if isinstance(path, str) else path
+    optim, _ = optim_of(_Files(f))
     P = O.OptimParams.from_cfg(optim)
     n_fg = f["obj_depth"].shape[0]
     dobs = np.concatenate([f["obj_depth"], np.zeros(f["obj_rays"].shape[0] - n_fg)])
@@ -75,6 +76,14 @@ def conditioning(path, d64, d32):
         worst.append(w)
     return {"perturbation": mags[:len(worst)], "worst_next_state_deviation": worst,
             "well_conditioned": bool(max(worst, default=0.0) <= CONTRACT)}
+
+
+class _Files(dict):
+    """a mapping with NpzFile's ``.files``, as optim_of reads it"""
+
+    def __init__(self, f):
+        super().__init__({k: f[k] for k in (f.files if hasattr(f, "files") else f.keys())})
+        self.files = list(self.keys())
 
 
 def decoders():

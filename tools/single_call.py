@@ -27,9 +27,15 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--pts", type=int, default=2048)
     a = ap.parse_args()
+    import ctypes
+
     from deep_sdf.workspace import decoder_from_state
+    from reconstruct import _libdsr as L
     from reconstruct.optimizer import Optimizer
     from reconstruct.utils import ForceKeyErrorDict
+
+    # an A/B against an older build (no trace records are used here): accept its ABI number
+    L.ABI_VERSION = ctypes.CDLL(L.lib_path()).dsr_abi_version()
 
     dec = decoder_from_state(S.make_decoder(1234), S.DEFAULT_SPECS, device=0)
     opt = Optimizer(dec, ForceKeyErrorDict(data_type="KITTI", optimizer=S.KITTI_OPTIM))
