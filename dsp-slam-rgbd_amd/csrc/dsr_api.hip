@@ -152,7 +152,7 @@ static JacKernel jac_kernel_for(const DevDecoder& D) {
 // swizzled H image (1496, default: 2-way instead of 4-way epilogue store conflicts,
 // bitwise equal to 472).  18 and 984 are timing experiments whose results are invalid, and
 // 216 (staggered groups with the scaled-weight epilogue) expired its bounded event waits
-// on some round-2 builds for a cause never isolated: all three exist only in
+// on some round-2 builds for a cause never isolated (git history, round 2-3): all three exist only in
 // a -DDSR_LITE_EXPERIMENTS build, never in the shipped library
 using LiteKernel = void (*)(DevDecoder, const Tile*, const int*, const ObjDesc*, const float4*, const float*,
                             const float*, float*, ErtArgs);
@@ -1125,10 +1125,9 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   }
   // Every group's slices of the per-ray / per-sample / per-point / per-slot buffers start on
   // a fresh 256 B line (zero padding between groups): the groups' kernels run concurrently on
-  // their own streams, and a cache line holding both groups' elements (the dead flags of the
-  // last rays of one group and the first of the next) was written by both at once — the
-  // run-to-run variable decode counts of DESIGN.md §3.9.  DSR_GROUP_ALIGN=0 (test hook) packs
-  // the groups back to back for that comparison.
+  // their own streams, so no cache line holds both groups' elements (round 5 suspected that for
+  // the variable decode counts of DESIGN.md §3.9; the cause was elsewhere, the layout stays).
+  // DSR_GROUP_ALIGN=0 (test hook) packs the groups back to back.
   bool galign = true;
   {
     const char* e = hook_env("DSR_GROUP_ALIGN");

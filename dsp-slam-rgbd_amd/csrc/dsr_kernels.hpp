@@ -1951,15 +1951,12 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // + s_damp on the scale, + k4 J_rot^T J_rot — so it is solved by a Cholesky factorisation
   // H = L L^T in fp64, with b carried as an extra row of L (row NPAR: the forward substitution
   // L y = b rides along in the factorisation) and one back substitution L^T dx = y: no pivot
-  // search, no row swaps, one barrier per column (the LU + explicit inverse
-  // it replaces took 63 + 21 us per solve).  dx is at least as accurate as the reference's fp32
+  // search, no row swaps, two barriers per 8-column panel (the LU + explicit
+  // inverse it replaces took 63 + 21 us per solve, this 40 + 6.5).  dx is at least as accurate as the reference's fp32
   // inverse-times-b (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_
   // the_reference holds it against fp64 truth).  A non-positive or NaN pivot (an H with NaN or
   // inf entries) falls back to the fp32 LU with partial pivoting below, the reference's own
   // getrf / getri arithmetic, so those cases behave exactly as before.
-#ifndef DSR_CHOL_VARIANT
-#define DSR_CHOL_VARIANT 4
-#endif
   constexpr int LP = NPAR + 3;                  // fp64 pitch 74: 16-byte aligned rows (the panel reads)
   __shared__ __attribute__((aligned(16))) double Lc[NPAR + 1][LP];
   __shared__ double rdg[NPAR];                  // 1 / L[c][c]
@@ -1970,46 +1967,12 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   }
   if (tid == 0) chol_bad = 0;
   __syncthreads();
-  // a double of lane 0 / lane k as a wave-uniform value (two v_readlane: no LDS round trip)
-  auto bcast0 = [](double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll)), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-  };
+  // a double of lane k as a wave-uniform value (two v_readlane: no LDS round trip)
   auto bcastk = [](double v, int k) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
   };
-  // column c of L from its updated values v (wave 0; lane l holds rows c + l and c + 64 + l):
-  // 1/sqrt(d) from v_rsq_f64 and two Newton steps (full fp64 precision), no sqrt / divide chain
-  auto chol_col = [&](int c, double v0, double v1) {
-    const int r0 = c + tid, r1 = r0 + 64;
-#if DSR_CHOL_VARIANT & 1
-    const double d2 = __shfl(v0, 0);
-    if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
-    const double dd = sqrt(d2);
-    if (r0 == c) {
-      Lc[c][c] = dd;
-      rdg[c] = 1.0 / dd;
-    }
-    else if (r0 <= NPAR) Lc[r0][c] = v0 / dd;
-    if (r1 <= NPAR) Lc[r1][c] = v1 / dd;
-#else
-    const double d2 = bcast0(v0);
-    if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
-    double rs = __builtin_amdgcn_rsq(d2);
-    rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
-    rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
-    if (r0 == c) {
-      Lc[c][c] = d2 * rs;
-      rdg[c] = rs;
-    }
-    else if (r0 <= NPAR) Lc[r0][c] = v0 * rs;
-    if (r1 <= NPAR) Lc[r1][c] = v1 * rs;
-#endif
-  };
-#if DSR_CHOL_VARIANT >= 4
   // Blocked right-looking Cholesky, panels of CPW columns: wave 0 factors a panel in registers
   // (lane l holds rows c0 + l and c0 + 64 + l; the pivot value and the panel's L[c'][c] reach the
   // other lanes by v_readlane), then all waves apply the panel to the trailing triangle (rows and
@@ -2096,56 +2059,6 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     }
     __syncthreads();
   }
-#else
-  if (tid < 64) chol_col(0, Lc[tid][0], 64 + tid <= NPAR ? Lc[64 + tid][0] : 0.0);
-  __syncthreads();
-  for (int k = 0; k + 1 < NPAR; ++k) {
-    if (tid < 64) {            // column k+1: its update by column k, then its scaling (look-ahead)
-      const int c = k + 1, r0 = c + tid, r1 = r0 + 64;
-      const double lck = Lc[c][k];
-      const double v0 = r0 <= NPAR ? Lc[r0][c] - Lc[r0][k] * lck : 0.0;
-      const double v1 = r1 <= NPAR ? Lc[r1][c] - Lc[r1][k] * lck : 0.0;
-      chol_col(c, v0, v1);
-    } else {                   // the rest of the trailing update: columns k+2.., rows j.. NPAR
-#if DSR_CHOL_VARIANT & 2
-      const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15;
-      for (int i = k + 2 + rr; i <= NPAR; i += 16) {
-        const double lik = Lc[i][k];
-        for (int j = k + 2 + cc; j <= i && j < NPAR; j += 16) Lc[i][j] -= lik * Lc[j][k];
-      }
-#else
-      // thread (rr, cc) of a 16 x 16 grid: rows k+2+rr+16m, columns k+2+cc+16q (m, q < 5); every
-      // operand is loaded before the first update so the LDS round trips overlap, and an element
-      // outside the triangle reads / writes the padding column LP-1 of row 0 instead of branching
-      const int rr = (tid - 64) >> 4, cc = (tid - 64) & 15, b0 = k + 2;
-      constexpr int NB = (NPAR + 1 + 15) / 16;
-      double li[NB], lj[NB], a[NB][NB];
-      double* const pad = &Lc[0][LP - 1];
-#pragma unroll
-      for (int m = 0; m < NB; ++m) {
-        const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * m;
-        li[m] = *(i <= NPAR ? &Lc[i][k] : pad);
-        lj[m] = *(j < NPAR ? &Lc[j][k] : pad);
-      }
-#pragma unroll
-      for (int m = 0; m < NB; ++m)
-#pragma unroll
-        for (int q = 0; q <= m; ++q) {
-          const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * q;
-          a[m][q] = *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad);
-        }
-#pragma unroll
-      for (int m = 0; m < NB; ++m)
-#pragma unroll
-        for (int q = 0; q <= m; ++q) {
-          const int i = b0 + rr + 16 * m, j = b0 + cc + 16 * q;
-          *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad) = a[m][q] - li[m] * lj[q];
-        }
-#endif
-    }
-    __syncthreads();
-  }
-#endif
 #ifdef DSR_SOLVE_PROFILE
   const long long tp2 = wall_clock64();
 #endif
