@@ -1978,8 +1978,14 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // other lanes by v_readlane), then all waves apply the panel to the trailing triangle (rows and
   // columns >= c1, the b row included) — 2 barriers per panel instead of 1 per column.
   constexpr int CPW = 8;
+#ifdef DSR_SOLVE_PROFILE
+  long long t_pan = 0, t_upd = 0;
+#endif
   for (int c0 = 0; c0 < NPAR; c0 += CPW) {
     const int c1 = min(c0 + CPW, NPAR);
+#ifdef DSR_SOLVE_PROFILE
+    const long long tq0 = wall_clock64();
+#endif
     if (tid < 64) {
       const int r0 = c0 + tid, r1 = r0 + 64;
       double a0[CPW], a1[CPW];
@@ -2018,6 +2024,10 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       }
     }
     __syncthreads();
+#ifdef DSR_SOLVE_PROFILE
+    const long long tq1 = wall_clock64();
+    t_pan += tq1 - tq0;
+#endif
     // trailing update by the panel: A[i][j] -= sum_u L[i][c0+u] L[j][c0+u], c1 <= j <= i, j < NPAR,
     // in 4 x 4 element blocks (block row bi >= block column bj), one per thread: the 8 panel values
     // of its 4 rows and 4 columns are loaded once (16-byte reads) and reused across the block
@@ -2058,6 +2068,9 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       }
     }
     __syncthreads();
+#ifdef DSR_SOLVE_PROFILE
+    t_upd += wall_clock64() - tq1;
+#endif
   }
 #ifdef DSR_SOLVE_PROFILE
   const long long tp2 = wall_clock64();
@@ -2210,7 +2223,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   }
 #ifdef DSR_SOLVE_PROFILE                 // (tools: per-phase wall clock of block 0, 100 MHz ticks)
   const long long tp3 = wall_clock64();
-  if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2);
+  if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2, t_pan, t_upd);
 #endif
   if (tid < CODE) zbuf[o * CODE + tid] = z[tid] + P.lr * dx[NPOSE + tid];   // :194
   if (tid == 0) {
