@@ -1952,7 +1952,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // H = L L^T in fp64, with b carried as an extra row of L (row NPAR: the forward substitution
   // L y = b rides along in the factorisation) and one back substitution L^T dx = y: no pivot
   // search, no row swaps, two barriers per 8-column panel (the LU + explicit
-  // inverse it replaces took 63 + 21 us per solve, this 40 + 6.5).  dx is at least as accurate as the reference's fp32
+  // inverse it replaces took 63 + 21 us per solve, this 25 + 6.5).  dx is at least as accurate as the reference's fp32
   // inverse-times-b (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_
   // the_reference holds it against fp64 truth).  A non-positive or NaN pivot (an H with NaN or
   // inf entries) falls back to the fp32 LU with partial pivoting below, the reference's own
@@ -1987,41 +1987,47 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     const long long tq0 = wall_clock64();
 #endif
     if (tid < 64) {
-      const int r0 = c0 + tid, r1 = r0 + 64;
-      double a0[CPW], a1[CPW];
+      // the panel's W columns with W a compile-time width (CPW, or NPAR % CPW for the last
+      // panel): straight-line code, no per-column guards
+      auto panel = [&](auto WC) {
+        constexpr int W = decltype(WC)::value;
+        const int r0 = c0 + tid, r1 = r0 + 64;
+        double a0[W], a1[W];
 #pragma unroll
-      for (int u = 0; u < CPW; ++u) {
-        const int c = c0 + u;
-        a0[u] = (c < c1 && r0 <= NPAR && c <= r0) ? Lc[r0][c] : 0.0;
-        a1[u] = (c < c1 && r1 <= NPAR) ? Lc[r1][c] : 0.0;
-      }
+        for (int u = 0; u < W; ++u) {
+          a0[u] = (r0 <= NPAR && c0 + u <= r0) ? Lc[r0][c0 + u] : 0.0;
+          a1[u] = r1 <= NPAR ? Lc[r1][c0 + u] : 0.0;
+        }
+        bool bad = false;
 #pragma unroll
-      for (int u = 0; u < CPW; ++u) {
-        if (c0 + u < c1) {
-          const double d2 = bcastk(a0[u], u);                 // row c0 + u sits in lane u
-          if (tid == 0 && !(d2 > 0.0)) chol_bad = 1;
-          double rs = __builtin_amdgcn_rsq(d2);
-          rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
-          rs = rs * __builtin_fma(-0.5 * d2 * rs, rs, 1.5);
+        for (int u = 0; u < W; ++u) {
+          const double d2 = bcastk(a0[u], u);                   // row c0 + u sits in lane u
+          bad = bad || !(d2 > 0.0);
+          // 1/sqrt(d2): an fp32 seed (v_rsq_f32, 1 ulp) and two Newton steps in fp64
+          double rs = (double)__builtin_amdgcn_rsqf((float)d2);
+          const double hd = 0.5 * d2;
+          rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
+          rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
           a0[u] = (tid == u) ? d2 * rs : a0[u] * rs;
           a1[u] = a1[u] * rs;
-          if (tid == u) rdg[c0 + u] = rs;
+          if (tid == 0) rdg[c0 + u] = rs;
 #pragma unroll
-          for (int w = u + 1; w < CPW; ++w) {                   // the panel's later columns
-            if (c0 + w < c1) {
-              const double lwu = bcastk(a0[u], w);              // L[c0 + w][c0 + u]
-              a0[w] -= a0[u] * lwu;
-              a1[w] -= a1[u] * lwu;
-            }
+          for (int w = u + 1; w < W; ++w) {                     // the panel's later columns
+            const double lwu = bcastk(a0[u], w);                // L[c0 + w][c0 + u]
+            a0[w] -= a0[u] * lwu;
+            a1[w] -= a1[u] * lwu;
           }
         }
-      }
+        if (tid == 0 && bad) chol_bad = 1;
 #pragma unroll
-      for (int u = 0; u < CPW; ++u) {
-        const int c = c0 + u;
-        if (c < c1 && r0 <= NPAR && c <= r0) Lc[r0][c] = a0[u];
-        if (c < c1 && r1 <= NPAR) Lc[r1][c] = a1[u];
-      }
+        for (int u = 0; u < W; ++u) {
+          if (r0 <= NPAR && c0 + u <= r0) Lc[r0][c0 + u] = a0[u];
+          if (r1 <= NPAR) Lc[r1][c0 + u] = a1[u];
+        }
+      };
+      static_assert(NPAR % CPW == 7, "last panel width");
+      if (c1 - c0 == CPW) panel(std::integral_constant<int, CPW>{});
+      else panel(std::integral_constant<int, NPAR % CPW>{});
     }
     __syncthreads();
 #ifdef DSR_SOLVE_PROFILE
@@ -2032,9 +2038,10 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     // in 4 x 4 element blocks (block row bi >= block column bj), one per thread: the 8 panel values
     // of its 4 rows and 4 columns are loaded once (16-byte reads) and reused across the block
     {
+      // (after the last panel, c1 = NPAR, nothing is left: every other panel is CPW wide)
       const int nr = NPAR + 1 - c1, nb = (nr + 3) >> 2;
       const int t = tid;
-      if (t < nb * (nb + 1) / 2) {
+      if (c1 < NPAR && t < nb * (nb + 1) / 2) {
         int bi = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
         while (bi * (bi + 1) / 2 > t) --bi;
         while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
@@ -2052,18 +2059,30 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
             lj[m][u] = vj.x; lj[m][u + 1] = vj.y;
           }
         }
+        // the block's 16 elements: all loaded, then updated, then stored (no load waits behind a
+        // store to a possibly aliasing element); outside the triangle a thread reads / writes its
+        // own padding slot of row NPAR (columns NPAR..LP-1 are never read as data)
+        double acc[4][4];
+        double* const pad = &Lc[NPAR][NPAR + (tid & 1)];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int i = i0 + m, j = j0 + q;
-            if (i <= NPAR && j < NPAR && j <= i) {
-              double acc = Lc[i][j];
+            acc[m][q] = *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad);
+          }
 #pragma unroll
-              for (int u = 0; u < CPW; ++u)
-                if (c0 + u < c1) acc -= li[m][u] * lj[q][u];
-              Lc[i][j] = acc;
-            }
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < CPW; ++u) acc[m][q] -= li[m][u] * lj[q][u];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = i0 + m, j = j0 + q;
+            *((i <= NPAR && j < NPAR && j <= i) ? &Lc[i][j] : pad) = acc[m][q];
           }
       }
     }
