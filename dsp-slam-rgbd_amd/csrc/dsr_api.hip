@@ -273,6 +273,7 @@ struct dsr_batch {
     unsigned* sync = nullptr;
     RenderChunk* rchunks = nullptr;   // k_render_rays chunks of the group's objects
     int* ccnt = nullptr;              // render points per chunk
+    int* scnt = nullptr;              // chunked render passes: samples, in-ball samples per chunk
     int n_rch = 0;
   };
   std::vector<Group> groups;
@@ -287,6 +288,7 @@ struct dsr_batch {
   int* tr_i = nullptr;
   int* dead = nullptr;          // per-ray early-termination flags (k_sample_pass)
   int* rinfo = nullptr;         // per-ray in-ball run (first in-ball sample | count << 8), or -1
+  int* rwin = nullptr;          // per-ray window of the current render pass (k_sample_scan / _count)
   unsigned char* refine = nullptr;   // per-sample flags of the lite pass (dsr_mlp_lite.hpp)
   uint64_t *rbits = nullptr, *abits = nullptr;   // per-ray refined / audited sample bits (k_refine_scan)
   MaskArgs ma{nullptr, nullptr, nullptr, nullptr};   // kept masks of the exact re-decode
@@ -1210,6 +1212,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   ALLOC(b->dense, sizeof(float) * (size_t)cand_off);
   ALLOC(b->dead, sizeof(int) * (size_t)std::max(1, ray_off));
   ALLOC(b->rinfo, sizeof(int) * (size_t)std::max(1, ray_off));
+  ALLOC(b->rwin, sizeof(int) * (size_t)std::max(1, ray_off));
 #ifdef DSR_EXP_PROV
   {
     int* pa = nullptr;
@@ -1336,6 +1339,7 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     gr.n_rch = (int)rch.size();
     ALLOC(gr.rchunks, sizeof(RenderChunk) * rch.size());
     ALLOC(gr.ccnt, sizeof(int) * rch.size());
+    ALLOC(gr.scnt, 2 * sizeof(int) * rch.size());
     if (!rch.empty() &&
         hipMemcpy(gr.rchunks, rch.data(), sizeof(RenderChunk) * rch.size(), hipMemcpyHostToDevice) != hipSuccess) {
       dsr_batch_destroy(b);
@@ -1712,18 +1716,22 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       ert.diag = b->diag;
       DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
                                        (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
-      const bool pre = b->prescan && gr.n_rch > 0;
-      int pre_arg = pre ? 1 : 0;                 // k_sample_pass's `prescanned` for the first pass
-#ifdef DSR_EXP_PROV
-      if (pre && getenv("DSR_EXP_SCAN_NOCLEAR")) pre_arg = 3;   // the scan writes the runs only
-#endif
-      if (pre)                                   // the first pass's ray scan over the ray chunks
-        hipLaunchKernelGGL(k_sample_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                           b->M, pre_arg == 3 ? (int*)nullptr : b->dead, b->rinfo);
+      const bool chunked = b->prescan && gr.n_rch > 0;
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
-        hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
-                           b->passes[pz], b->passes[pz + 1], b->cand, b->dense, b->dead, b->rinfo,
-                           pz == 0 ? pre_arg : 0);
+        const int ra = b->passes[pz], rb = b->passes[pz + 1];
+        if (chunked) {                           // count (the first pass: the ray scan), then emit
+          if (pz == 0)
+            hipLaunchKernelGGL(k_sample_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                               b->M, rb, b->dead, b->rinfo, b->rwin, gr.scnt);
+          else
+            hipLaunchKernelGGL(k_sample_count, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                               b->M, ra, rb, b->dead, b->rinfo, b->rwin, gr.scnt);
+          hipLaunchKernelGGL(k_sample_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
+                             b->M, ra, rb, b->cand, b->rwin, gr.scnt);
+        } else {
+          hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
+                             ra, rb, b->cand, b->dead, b->rinfo);
+        }
         hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
                            b->lite ? LTILE : TILE, 0);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));

@@ -1,12 +1,13 @@
 // dsr_kernels.hpp — the device-resident Gauss-Newton iteration of
 // Optimizer.reconstruct_object (reconstruct/optimizer.py:90-205) for a batch of
-// independent objects.  One iteration = 6 + 3 x (render passes) launches, none of which
+// independent objects.  One iteration = 8 + 4 x (render passes) launches, none of which
 // needs the host:
 //
 //   k_iter_begin   optimizer.py:122-128  t_cam_obj, scale, linspace depths, bg depth,
 //                                        + code folded into lin0 / lin4 biases
 //   per render pass (early ray termination, exact — see k_sample_pass):
-//   k_sample_pass  loss.py:71-88         ray samples -> object frame -> |x|<1 ->
+//   k_sample_scan / k_sample_count + k_sample_emit
+//                  loss.py:71-88         ray samples -> object frame -> |x|<1 ->
 //                                        (ray, depth)-ordered compaction of live rays
 //   k_tiles_fwd    —                     64-point tiles over the pass's samples
 //   k_mlp_fwd      loss.py:91-92         decode_sdf (MFMA), flags terminated rays
@@ -16,7 +17,7 @@
 //   k_mlp_jac      loss.py:22-43,157-164 fwd + analytic input Jacobian (MFMA), Sim(3)
 //                  loss_utils.py:176-195 point Jacobian, Huber (loss_utils.py:246-275),
 //                  optimizer.py:163-169  per-tile J^T J, J^T r~, sum r~^2
-//   k_solve        optimizer.py:131-194  reduce, damp, rotation prior, fp32 LU inverse,
+//   k_solve        optimizer.py:131-194  reduce, damp, rotation prior, fp64 Cholesky solve,
 //                                        exp_sim3, pose/code update, failure exits
 #pragma once
 #include "dsr_dev.hpp"
@@ -266,6 +267,10 @@ __global__ __launch_bounds__(512) void k_iter_begin(int n_obj, const ObjDesc* __
     S.k = 0;
     S.n_emit = S.n_eval = S.n_refine = 0;
     S.n_audit = S.lite_viol = 0;
+    if (desc[o].n_rays == 0) {                          // no in-ball samples: loss.py:86-88 (the
+      S.status = ST_FAIL;                               // chunked render passes have no workgroup
+      S.fail_reason = DSR_FAIL_RENDER_FEW;              // for a ray-less object to fail it in)
+    }
     if (S.lite_redo) {                                  // an audit caught a misclassification:
       S.lite_margin = 1e30f;                            // every sample exact from now on
     } else if (S.iters_done == 0) {
@@ -311,7 +316,7 @@ __device__ __forceinline__ float3 ray_sample(const float3 r, const SampleLds& L,
 }
 
 // ------------------------------------------------------------------------------------
-// k_sample_pass: the ray samples of loss.py:71-82, emitted in render passes with early
+// Render passes: the ray samples of loss.py:71-82, emitted in render passes with early
 // ray termination.  Pass [ra, rb) emits, for every ray not yet flagged dead, its
 // in-ball samples of in-ball rank ra..rb-1 (rank = position among the ray's in-ball
 // samples, depth order).  `dense` is NaN-filled before the first pass (out-of-ball samples
@@ -323,7 +328,7 @@ __device__ __forceinline__ float3 ray_sample(const float3 r, const SampleLds& L,
 // any output, and k_render sees it only behind T == 0.  Results are bit-identical to
 // decoding every in-ball sample; the first pass also marks the out-of-ball samples (NaN)
 // and counts n_valid (loss.py:82-88) over ALL in-ball samples.
-// One thread per ray, one workgroup per object, (ray, depth)-ordered output.
+// One thread per ray, (ray, depth)-ordered output (k_sample_scan / _count / _emit below).
 // ------------------------------------------------------------------------------------
 // Ray chunks: k_refine_* and k_render_* run one workgroup per RENDER_RAYS rays of an object
 // (table built once per batch), so an object's rays are processed side by side.
@@ -345,20 +350,62 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
-// k_sample_scan: the first render pass's per-ray scan (each ray's in-ball run, loss.py:82; its
-// dead flag cleared) spread over the object group's 128-ray chunks, one thread per ray, instead
-// of one 1024-thread workgroup per object walking its rays in rounds; k_sample_pass then emits
-// the first window from the runs as later passes do.  Launched per object group with the
+// Chunked render passes (one thread per ray, one workgroup per RENDER_RAYS rays of an object,
+// the render chunk table): a pass is a count kernel — k_sample_scan for the first pass, which
+// also records each ray's in-ball run (loss.py:82) and clears its dead flag, k_sample_count for
+// later passes — then k_sample_emit, which places every chunk at the sum of the earlier chunks'
+// counts: the (ray, depth)-ordered list k_sample_pass's one workgroup per object builds, spread
+// over the CUs (one KITTI object: 18 workgroups instead of one).  Per ray the count kernel leaves
+// rwin = cnt | (j0 + 1) << 8 (j0 = the ray's first in-ball sample, -1 when its in-ball set is not
+// one run: k_sample_emit then walks the ray); per chunk sc[2c] = samples emitted, sc[2c + 1] =
+// in-ball samples (first pass: n_valid, loss.py:82-88).  Launched per object group with the
 // group's own descriptor / state slices and chunk table (RenderChunk.obj is group-relative), so
 // no workgroup touches another group's rays.
-// (no packed-FP32 VALU ops in this kernel, nor in the other two that form ray samples,
-// k_sample_pass and k_refine_emit: DESIGN.md §3.9 — under concurrent decoder kernels the
-// SLP-paired v_pk_mul_f32 of this loop's first trip returned wrong products in one quarter-wave)
+// (no packed-FP32 VALU ops in the kernels that form ray samples — k_sample_scan / _count /
+// _emit / _pass and k_refine_emit: DESIGN.md §3.9 — under concurrent decoder kernels the
+// SLP-paired v_pk_mul_f32 of the scan loop's first trip returned wrong products in one quarter-wave)
+__device__ __forceinline__ void chunk_sums(int a, int b, int* __restrict__ out) {
+  __shared__ int ws[2][RENDER_RAYS / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 32; k > 0; k >>= 1) {
+    a += __shfl_xor(a, k);
+    b += __shfl_xor(b, k);
+  }
+  if (lane == 0) { ws[0][wv] = a; ws[1][wv] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int x = 0, y = 0;
+    for (int k = 0; k < RENDER_RAYS / 64; ++k) { x += ws[0][k]; y += ws[1][k]; }
+    out[0] = x;
+    out[1] = y;
+  }
+}
+
+// The in-ball samples of ranks [ra, rb) of a ray whose in-ball set is not one run (rank =
+// position among the ray's in-ball samples, depth order): their number, and the ray's in-ball
+// total when the walk is not cut at rb.
+__device__ __forceinline__ int walk_count(const float3 rv, const SampleLds& L, int M, int ra, int rb,
+                                          bool cut, int& nin) {
+  int rank = 0, cnt = 0;
+  for (int j = 0; j < M; ++j) {
+    const float3 x = ray_sample(rv, L, j);
+    const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+    if (!(nrm < 1.0f)) continue;                                      // loss.py:82
+    if (rank >= ra && rank < rb) ++cnt;
+    ++rank;
+    if (cut && rank >= rb) break;
+  }
+  nin = rank;
+  return cnt;
+}
+
 __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_scan(const RenderChunk* __restrict__ chunks,
                                                              const ObjDesc* __restrict__ desc,
                                                              const ObjState* __restrict__ st,
-                                                             const float* __restrict__ rays_all, int M,
-                                                             int* __restrict__ dead, int* __restrict__ rinfo) {
+                                                             const float* __restrict__ rays_all, int M, int rb,
+                                                             int* __restrict__ dead, int* __restrict__ rinfo,
+                                                             int* __restrict__ rwin, int* __restrict__ sc) {
   const RenderChunk ch = chunks[blockIdx.x];
   const ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
@@ -370,54 +417,153 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_scan(const
   if (threadIdx.x == 0) prov_state(1, S.iters_done, d.ray_off + ch.ray0, prov_sum(L.T, L.depths, M));
 #endif
   const int ray = ch.ray0 + threadIdx.x;
-  if (ray >= d.n_rays) return;
-  const float* rays = rays_all + (size_t)d.ray_off * 3;
-  const float3 rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
-  if (dead) {                     // (nullptr: k_sample_pass clears the flags, DSR_EXP_SCAN_NOCLEAR)
+  int cnt = 0, rank = 0;
+  if (ray < d.n_rays) {
+    const float* rays = rays_all + (size_t)d.ray_off * 3;
+    const float3 rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
     dead_put(dead + d.ray_off + ray, 0);
 #ifdef DSR_EXP_PROV
     prov_clear(S.iters_done, d.ray_off + ray);
 #endif
-  }
-  int rank = 0, jf = -1, jl = -1;
-#ifdef DSR_EXP_PROV
-  float pn[4] = {0.f, 0.f, 0.f, 0.f};
-#endif
-  for (int j = 0; j < M; ++j) {
-    const float3 x = ray_sample(rv, L, j);
-    const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
-#ifdef DSR_EXP_PROV
-    if (j < 4) pn[j] = nrm;
-#endif
-    if (!(nrm < 1.0f)) continue;
-    if (jf < 0) jf = j;
-    jl = j;
-    ++rank;
-  }
-#ifdef DSR_EXP_PROV
-  if (g_prov_nrm && S.iters_done < PROV_IT) {
-    float* q = g_prov_nrm + ((size_t)S.iters_done * g_prov_R + d.ray_off + ray) * 12;
-    for (int j = 0; j < 4; ++j) {
+    int jf = -1, jl = -1;
+    for (int j = 0; j < M; ++j) {
       const float3 x = ray_sample(rv, L, j);
-      q[j] = pn[j];
-      q[4 + j] = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
-      q[8 + j] = L.depths[j];
+      const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+      if (!(nrm < 1.0f)) continue;
+      if (jf < 0) jf = j;
+      jl = j;
+      ++rank;
     }
-  }
-#endif
-  rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
+    // the in-ball set of a ray is one run of samples unless rounding makes |x| < 1 flicker
+    // near a tangent point; such rays are walked again in every pass
+    const int info = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
+    rinfo[d.ray_off + ray] = info;
+    cnt = min(rank, rb);
+    const int j0 = info >= 0 ? (info & 255) : -1;
+    rwin[d.ray_off + ray] = cnt | ((j0 + 1) << 8);
 #ifdef DSR_EXP_PROV
-  prov_rinfo(0, S.iters_done, d.ray_off + ray, rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1));
+    prov_rinfo(0, S.iters_done, d.ray_off + ray, info);
+    prov_alive(S.iters_done, 0, d.ray_off + ray, cnt + 1);
+    prov_emit(S.iters_done, 0, d.ray_off + ray, cnt > 0 ? (j0 >= 0 ? j0 : -2) : -1);
 #endif
+  }
+  chunk_sums(cnt, rank, sc + 2 * blockIdx.x);
 }
 
-// prescanned: bit 0 — the first pass's runs (and, without bit 1, its cleared dead flags) come
-// from k_sample_scan; bit 1 (diagnostic builds) — the first pass clears the flags itself
+// later passes [ra, rb): the rays not flagged dead by the earlier passes' decodes
+__global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_count(const RenderChunk* __restrict__ chunks,
+                                                              const ObjDesc* __restrict__ desc,
+                                                              const ObjState* __restrict__ st,
+                                                              const float* __restrict__ rays_all, int M, int ra,
+                                                              int rb, int* __restrict__ dead,
+                                                              const int* __restrict__ rinfo,
+                                                              int* __restrict__ rwin, int* __restrict__ sc) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  const ObjState& S = st[ch.obj];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[ch.obj];
+  __shared__ SampleLds L;
+  stage_samples(L, S, M, threadIdx.x);
+  __syncthreads();
+  const int ray = ch.ray0 + threadIdx.x;
+  int cnt = 0;
+  if (ray < d.n_rays) {
+    const bool alive = dead_get(dead + d.ray_off + ray) == 0;
+    int j0 = -1;
+    if (alive) {
+      const int info = rinfo[d.ray_off + ray];
+      if (info >= 0) {
+        j0 = info & 255;
+        cnt = max(0, min(rb, info >> 8) - ra);
+      } else {
+        const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
+        int nin;
+        cnt = walk_count(make_float3(rp[0], rp[1], rp[2]), L, M, ra, rb, true, nin);
+      }
+    }
+    rwin[d.ray_off + ray] = cnt | ((j0 + 1) << 8);
+#ifdef DSR_EXP_PROV
+    prov_alive(S.iters_done, ra, d.ray_off + ray, alive ? cnt + 1 : -1);
+    prov_emit(S.iters_done, ra, d.ray_off + ray, cnt > 0 ? (j0 >= 0 ? j0 + ra : -2) : -1);
+#endif
+  }
+  chunk_sums(cnt, 0, sc + 2 * blockIdx.x);
+}
+
+__global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_emit(const RenderChunk* __restrict__ chunks,
+                                                             const ObjDesc* __restrict__ desc, ObjState* st,
+                                                             const float* __restrict__ rays_all, int M, int ra,
+                                                             int rb, float4* __restrict__ cand,
+                                                             const int* __restrict__ rwin,
+                                                             const int* __restrict__ sc) {
+  const RenderChunk ch = chunks[blockIdx.x];
+  ObjState& S = st[ch.obj];
+  if (S.status != ST_RUNNING) return;
+  const ObjDesc d = desc[ch.obj];
+  __shared__ int wsum[RENDER_RAYS / 64];
+  __shared__ SampleLds L;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  stage_samples(L, S, M, tid);
+  int base = 0;
+  for (int c = ch.first; c < (int)blockIdx.x; ++c) base += sc[2 * c];
+  const int ray = ch.ray0 + tid;
+  int cnt = 0, j0 = -1;
+  float3 rv = make_float3(0.f, 0.f, 0.f);
+  if (ray < d.n_rays) {
+    const int w = rwin[d.ray_off + ray];
+    cnt = w & 255;
+    j0 = (w >> 8) - 1;
+    if (cnt > 0) {
+      const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
+      rv = make_float3(rp[0], rp[1], rp[2]);
+    }
+  }
+  const int inc = wave_incl_scan(cnt, lane);
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int off = d.cand_off + base + inc - cnt;
+  for (int k = 0; k < wv; ++k) off += wsum[k];
+  if (cnt > 0 && j0 >= 0) {
+    for (int k = ra; k < ra + cnt; ++k) {
+      const float3 x = ray_sample(rv, L, j0 + k);
+      cand[off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j0 + k));
+    }
+  } else if (cnt > 0) {
+    int rank = 0;
+    for (int j = 0; j < M && rank < rb; ++j) {
+      const float3 x = ray_sample(rv, L, j);
+      const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
+      if (!(nrm < 1.0f)) continue;
+      if (rank >= ra) cand[off++] = make_float4(x.x, x.y, x.z, __int_as_float(ray * M + j));
+      ++rank;
+    }
+  }
+  if (tid == 0 && (int)blockIdx.x == ch.first + ch.n - 1) {   // the object's last chunk: its totals
+    int t = base;
+    for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
+    S.n_emit = t;
+    S.n_eval += t;
+    if (ra == 0) {
+      int nin = 0;
+      for (int c = ch.first; c <= (int)blockIdx.x; ++c) nin += sc[2 * c + 1];
+      S.n_valid = nin;
+      if (nin < 10) {                          // loss.py:86-88 -> optimizer.py:144-145
+        S.status = ST_FAIL;
+        S.fail_reason = DSR_FAIL_RENDER_FEW;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_sample_pass: the same pass in one 1024-thread workgroup per object walking its rays in
+// rounds (DSR_PRESCAN=0: the schedule tests' second implementation of the pass), first pass
+// included: it clears the dead flags, records the runs and counts n_valid itself.
+// ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SAMPLE_THREADS) DSR_NO_PK_F32 void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
                                                                 ObjState* st, const float* __restrict__ rays_all,
                                                                 int M, int ra, int rb, float4* __restrict__ cand,
-                                                                float* __restrict__ dense, int* __restrict__ dead,
-                                                                int* __restrict__ rinfo, int prescanned) {
+                                                                int* __restrict__ dead, int* __restrict__ rinfo) {
   const int o = blockIdx.x;
   ObjState& S = st[o];
   if (S.status != ST_RUNNING) return;
@@ -435,70 +581,39 @@ __global__ __launch_bounds__(SAMPLE_THREADS) DSR_NO_PK_F32 void k_sample_pass(in
   for (int r0 = 0; r0 < d.n_rays; r0 += SAMPLE_THREADS) {
     const int ray = r0 + tid;
     int cnt = 0, nin = 0;
-    bool alive = false;
     int j0 = -1;                  // later passes: the ray's in-ball samples are j0 .. j0+nin-1
     float3 rv = make_float3(0.f, 0.f, 0.f);
     if (ray < d.n_rays) {
       rv = make_float3(rays[ray * 3 + 0], rays[ray * 3 + 1], rays[ray * 3 + 2]);
-      if (first && (prescanned & 1) == (prescanned >> 1)) {   // 0 (no scan) or 3
-        dead_put(dead + d.ray_off + ray, 0);
-#ifdef DSR_EXP_PROV
-        prov_clear(S.iters_done, d.ray_off + ray);
-#endif
-      }
-      alive = first || dead_get(dead + d.ray_off + ray) == 0;
-      if (alive && (!first || prescanned)) {
+      if (first) dead_put(dead + d.ray_off + ray, 0);
+      const bool alive = first || dead_get(dead + d.ray_off + ray) == 0;
+      if (alive && !first) {
         const int info = rinfo[d.ray_off + ray];
-#ifdef DSR_EXP_PROV
-        if (first) prov_rinfo(1, S.iters_done, d.ray_off + ray, info);
-#endif
-        if (info >= 0) {          // contiguous in-ball run (first pass): the window directly
+        if (info >= 0) {          // contiguous in-ball run: the window directly
           j0 = info & 255;
           nin = info >> 8;
           cnt = max(0, min(rb, nin) - ra);
         }
       }
       if (alive && j0 < 0) {
-        int rank = 0, jf = -1, jl = -1;
-#ifdef DSR_EXP_PROV
-        float pn[4] = {0.f, 0.f, 0.f, 0.f};
-#endif
-        for (int j = 0; j < M; ++j) {
-          const float3 x = ray_sample(rv, L, j);
-          const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
-#ifdef DSR_EXP_PROV
-          if (j < 4) pn[j] = nrm;
-#endif
-          if (!(nrm < 1.0f)) continue;   // loss.py:82 (out of ball: NaN, dense pre-filled)
-          if (jf < 0) jf = j;
-          jl = j;
-          if (rank >= ra && rank < rb) ++cnt;
-          ++rank;
-          if (!first && rank >= rb) break;
-        }
-        nin = rank;
-#ifdef DSR_EXP_PROV
-        if (first && g_prov_nrm2 && S.iters_done < PROV_IT) {
-          float* q = g_prov_nrm2 + ((size_t)S.iters_done * g_prov_R + d.ray_off + ray) * 8;
-          for (int j = 0; j < 4; ++j) {
+        if (first) {
+          int rank = 0, jf = -1, jl = -1;
+          for (int j = 0; j < M; ++j) {
             const float3 x = ray_sample(rv, L, j);
-            q[j] = pn[j];
-            q[4 + j] = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);
+            const float nrm = sqrtf((x.x * x.x + x.y * x.y) + x.z * x.z);   // torch.norm(.., dim=-1)
+            if (!(nrm < 1.0f)) continue;   // loss.py:82 (out of ball: NaN, dense pre-filled)
+            if (jf < 0) jf = j;
+            jl = j;
+            if (rank < rb) ++cnt;
+            ++rank;
           }
-        }
-#endif
-        // the in-ball set of a ray is one run of samples unless rounding makes |x| < 1
-        // flicker near a tangent point; such rays keep scanning in every pass
-        if (first && !prescanned)
+          nin = rank;
           rinfo[d.ray_off + ray] = rank == 0 ? 0 : (jl - jf + 1 == rank ? (jf | (rank << 8)) : -1);
+        } else {
+          cnt = walk_count(rv, L, M, ra, rb, true, nin);
+        }
       }
     }
-#ifdef DSR_EXP_PROV
-    if (ray < d.n_rays) {
-      prov_alive(S.iters_done, ra, d.ray_off + ray, alive ? cnt + 1 : -1);
-      prov_emit(S.iters_done, ra, d.ray_off + ray, cnt > 0 ? (j0 >= 0 ? j0 + ra : -2) : -1);
-    }
-#endif
     const int inc = wave_incl_scan(cnt, lane);
     int nin_w = nin;
 #pragma unroll
@@ -581,11 +696,12 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
   // that is certainly full, or up to and including it when it is an audited full sample
   // (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag) ride along in bit 30 of
   // the candidate's index so the exact pass can check their class.
-  for (int i0 = 0; i0 < 64; i0 += 8) {     // 8 rays' loads in flight
-    unsigned char fv[8];
-    float yv[8];
+  constexpr int NIF = 32;                  // rays' loads in flight per wave
+  for (int i0 = 0; i0 < 64; i0 += NIF) {
+    unsigned char fv[NIF];
+    float yv[NIF];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < NIF; ++u) {
       const int rr = ch.ray0 + 64 * wv + i0 + u;
       const bool in = rr < d.n_rays && lane < M;
       const size_t e = d.cand_off + (size_t)rr * M + lane;
@@ -593,7 +709,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
       yv[u] = (in && dense) ? dense[e] : __builtin_nanf("");
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < NIF; ++u) {
       const int rr = ch.ray0 + 64 * wv + i0 + u;
       const uint64_t fb = __ballot(fv[u] != 0);
       const uint64_t ub = __ballot((fv[u] == 0 || fv[u] == 3) && yv[u] <= full);
@@ -917,16 +1033,18 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   if (tid < M) dep_s[tid] = S.depths[tid];
   const int nr = min(RENDER_RAYS, d.n_rays - ch.ray0);
   {
-    // element e -> (row e / M, column e % M) advanced without per-element divisions; four
-    // loads in flight per thread before their LDS stores
+    // element e -> (row e / M, column e % M) advanced without per-element divisions; 16
+    // loads in flight per thread before their LDS stores (a chunk's 128 x M values in ~4
+    // rounds of load latency: the staging was most of this kernel's time with 4)
+    constexpr int NLD = 16;
     const float* src = dense + d.cand_off + (size_t)ch.ray0 * M;
     const int tot = nr * M, sq = RENDER_RAYS / M, sr = RENDER_RAYS - sq * M;
     int r = tid / M, j = tid - r * M;
-    for (int e = tid; e < tot; e += 4 * RENDER_RAYS) {
-      float v[4];
-      int o[4];
+    for (int e = tid; e < tot; e += NLD * RENDER_RAYS) {
+      float v[NLD];
+      int o[NLD];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < NLD; ++u) {
         v[u] = (e + u * RENDER_RAYS < tot) ? src[e + u * RENDER_RAYS] : 0.f;
         o[u] = r * pitch + j;
         j += sr;
@@ -934,7 +1052,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
         if (j >= M) { j -= M; ++r; }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < NLD; ++u)
         if (e + u * RENDER_RAYS < tot) {
           T_s[o[u]] = v[u];
           D_s[o[u]] = v[u];
@@ -945,7 +1063,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   const float dmax = S.dmax, delta_d = S.delta_d;
   const int ray = ch.ray0 + tid;
   float* Tr = T_s + tid * pitch;
-  const float* Dr = D_s + tid * pitch;
+  float* Dr = D_s + tid * pitch;                  // sdf row; a kept sample's slot then holds its de_do
   int cnt = 0, jend = 0;
   float du = 0.f, dob = 0.f;
   uint64_t keep = 0;
@@ -979,7 +1097,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
       double sacc = 0.0;
       for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
       const float dedo = (float)sacc / (1.f - occupancy(Dr[jj], nth, th, two_th));   // :131-132
-      if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; }                              // :135
+      if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; Dr[jj] = dedo; }              // :135
     }
   }
   const int inc = wave_incl_scan(cnt, lane);
@@ -996,9 +1114,7 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
     const size_t base = (size_t)d.cand_off + (size_t)ch.ray0 * M;
     for (uint64_t m = keep; m; m &= m - 1) {
       const int jj = __builtin_ctzll(m);
-      double sacc = 0.0;
-      for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
-      const float dedo = (float)sacc / (1.f - occupancy(Dr[jj], nth, th, two_th));
+      const float dedo = Dr[jj];
       const float deds = (dedo * delta_d) * do_ds;    // :142
       const float dj = dep_s[jj];
       const float3 x = xform(S.T, rx * dj, ry * dj, rz * dj);   // = ray_sample(rays, S, ray, jj)
@@ -1873,17 +1989,42 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   __shared__ int piv[NPAR];
   __shared__ float pivv[NPAR];
   __shared__ int flag;
+  constexpr int LP = NPAR + 3;                  // fp64 pitch 74: 16-byte aligned rows (the panel reads)
+  __shared__ __attribute__((aligned(16))) double Lc[NPAR + 1][LP];   // Cholesky factor, b as row NPAR
+  __shared__ double rdg[NPAR];                  // 1 / L[c][c]
+  __shared__ int chol_bad;
 #ifdef DSR_SOLVE_PROFILE
   const long long tp0 = wall_clock64();
 #endif
-  {   // the tile partials' sums (k_reduce_slots)
+  {   // the tile partials' sums (k_reduce_slots): all of a thread's loads issued before its stores
+    constexpr int NL = (SLOT_FLOATS + SOLVE_THREADS - 1) / SOLVE_THREADS;
     const float* r = red + (size_t)o * SRED_STRIDE;
-    for (int e = tid; e < SLOT_FLOATS; e += SOLVE_THREADS) {
-      Ss[e] = r[e];
-      Sr[e] = r[SLOT_FLOATS + e];
+    float vs[NL], vr[NL];
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int e = min(tid + q * SOLVE_THREADS, SLOT_FLOATS - 1);
+      vs[q] = r[e];
+      vr[q] = r[SLOT_FLOATS + e];
+    }
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int e = tid + q * SOLVE_THREADS;
+      if (e < SLOT_FLOATS) {
+        Ss[e] = vs[q];
+        Sr[e] = vr[q];
+      }
     }
   }
   if (tid < CODE) z[tid] = zbuf[o * CODE + tid];
+  // rotation prior, loss.py:169-192, at the current (pre-update) pose (rotation_prior), by a
+  // lane of wave 1 while the loads land (its result is only read when no failure exit is taken)
+  if (tid == 64) {
+#ifdef DSR_EXP_PRIOR_FP32
+    scal[1] = rotation_prior_fp32(S.Tco, jrot);
+#else
+    scal[1] = rotation_prior(S.Tco, jrot);
+#endif
+  }
   __syncthreads();
   const int it = S.iters_done;
   if (tid == 0) {
@@ -1901,12 +2042,6 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       S.fail_reason = f;
     } else {
       scal[0] = P.k1 * ren_loss + P.k2 * sdf_loss;                 // :157
-      // rotation prior, loss.py:169-192, at the current (pre-update) pose (rotation_prior)
-#ifdef DSR_EXP_PRIOR_FP32
-      scal[1] = rotation_prior_fp32(S.Tco, jrot);
-#else
-      scal[1] = rotation_prior(S.Tco, jrot);
-#endif
       scal[2] = N;
       scal[3] = K;
     }
@@ -1929,20 +2064,22 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
         if (a == NPOSE - 1 && b == NPOSE - 1) h = h + P.s_damp;
       }
       A[a][b] = h;
+      if (b <= a) Lc[a][b] = (double)h;        // the Cholesky's working copy (lower triangle)
     }
     for (int a = tid; a < NPAR; a += SOLVE_THREADS) {
       float v = ((-k1) * Sr[NTRI + a]) / K + ((-k2) * Ss[NTRI + a]) / N;
       if (a >= NPOSE) v = v - k3 * z[a - NPOSE];
       else v = v - k4 * (-(jrot[a] * scal[1]));
       bv[a] = v;
+      Lc[NPAR][a] = (double)v;                 // b as row NPAR
     }
+    if (tid == 0) chol_bad = 0;
   }
   __syncthreads();
   if (trace_H) {
     for (int e = tid; e < NPAR * NPAR; e += SOLVE_THREADS)
       trace_H[((size_t)it * stride + o) * TRACE_H_STRIDE + e] = A[e / NPAR][e % NPAR];
   }
-  __syncthreads();
 #ifdef DSR_SOLVE_PROFILE
   const long long tp1 = wall_clock64();
 #endif
@@ -1957,16 +2094,6 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // the_reference holds it against fp64 truth).  A non-positive or NaN pivot (an H with NaN or
   // inf entries) falls back to the fp32 LU with partial pivoting below, the reference's own
   // getrf / getri arithmetic, so those cases behave exactly as before.
-  constexpr int LP = NPAR + 3;                  // fp64 pitch 74: 16-byte aligned rows (the panel reads)
-  __shared__ __attribute__((aligned(16))) double Lc[NPAR + 1][LP];
-  __shared__ double rdg[NPAR];                  // 1 / L[c][c]
-  __shared__ int chol_bad;
-  for (int e = tid; e < (NPAR + 1) * NPAR; e += SOLVE_THREADS) {
-    const int a = e / NPAR, b = e - (e / NPAR) * NPAR;
-    if (b <= a) Lc[a][b] = (double)(a < NPAR ? A[a][b] : bv[b]);
-  }
-  if (tid == 0) chol_bad = 0;
-  __syncthreads();
   // a double of lane k as a wave-uniform value (two v_readlane: no LDS round trip)
   auto bcastk = [](double v, int k) {
     const long long b = __double_as_longlong(v);
@@ -2096,16 +2223,27 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
 #endif
   if (!chol_bad) {
     if (tid < 64) {            // L^T dx = y (row NPAR of L), one dependent step per row, wave 0
+      // every L value a lane will use is loaded first (its column of L^T and 1 / L[r][r]), so
+      // the dependent chain per row is register-only: x_k = y_k / L[k][k] on lane k, v_readlane,
+      // one fma per lane
       const int r0 = tid, r1 = tid + 64;
+      constexpr int N1 = NPAR - 64;
+      double l0[NPAR], l1[N1];
+#pragma unroll
+      for (int kk = 0; kk < NPAR; ++kk) l0[kk] = Lc[kk][r0];
+#pragma unroll
+      for (int kk = 0; kk < N1; ++kk) l1[kk] = Lc[64 + kk][min(r1, NPAR - 1)];
+      const double d0 = rdg[r0], d1 = rdg[min(r1, NPAR - 1)];
       double y0 = Lc[NPAR][r0], y1 = r1 < NPAR ? Lc[NPAR][r1] : 0.0;
 #pragma unroll
       for (int kk = NPAR - 1; kk >= 0; --kk) {
-        const double yk = kk < 64 ? bcastk(y0, kk) : bcastk(y1, kk - 64);
-        const double xk = yk * rdg[kk];
+        const double xk = kk < 64 ? bcastk(y0 * d0, kk) : bcastk(y1 * d1, kk - 64);
         if (r0 == kk) y0 = xk;
-        else if (r0 < kk) y0 -= Lc[kk][r0] * xk;
-        if (r1 == kk) y1 = xk;
-        else if (r1 < kk) y1 -= Lc[kk][r1] * xk;
+        else if (r0 < kk) y0 -= l0[kk] * xk;
+        if (kk >= 64) {
+          if (r1 == kk) y1 = xk;
+          else if (r1 < kk) y1 -= l1[kk - 64] * xk;
+        }
       }
       dx[r0] = (float)y0;
       if (r1 < NPAR) dx[r1] = (float)y1;
