@@ -1747,7 +1747,7 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       const bool rays = gr.n_rch > 0;            // (a group of ray-less objects: all failed, loss.py:86-88)
       if (b->lite) {                             // exact split-fp16 decode of the band samples
         if (rays) {
-          hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->M,
+          hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(REFINE_SCAN_THREADS), 0, s, gr.rchunks, desc, st, b->M,
                              b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt,
                              b->ma.slotmap);
           hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,

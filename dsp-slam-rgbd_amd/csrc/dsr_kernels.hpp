@@ -676,7 +676,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) DSR_NO_PK_F32 void k_sample_pass(in
 // samples hold NaN, so the scan reads only this iteration's values.  `dense` == nullptr
 // refines every flagged sample (DSR_REFINE_ALL=1).
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* __restrict__ chunks,
+constexpr int REFINE_SCAN_THREADS = 256;   // 4 waves x 32 rays of a chunk: one round of loads each
+__global__ __launch_bounds__(REFINE_SCAN_THREADS) void k_refine_scan(const RenderChunk* __restrict__ chunks,
                                                              const ObjDesc* __restrict__ desc, ObjState* st,
                                                              int M, unsigned char* __restrict__ refine,
                                                              const float* __restrict__ dense, float nth,
@@ -687,30 +688,30 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
   const ObjDesc d = desc[ch.obj];
+  constexpr int NW = REFINE_SCAN_THREADS / 64, RPW = RENDER_RAYS / NW;   // waves, rays per wave
   __shared__ uint64_t rbits[RENDER_RAYS], abits[RENDER_RAYS];
-  __shared__ int wsum[RENDER_RAYS / 64];
+  __shared__ int wsum[2][NW];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float full = nth - S.lite_margin;
-  // Each wave scans its 64 rays one at a time, lane j on sample j (coalesced flag / value
-  // loads, ballots): refined = the flagged samples in front of the first unflagged sample
-  // that is certainly full, or up to and including it when it is an audited full sample
-  // (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag) ride along in bit 30 of
-  // the candidate's index so the exact pass can check their class.
-  constexpr int NIF = 32;                  // rays' loads in flight per wave
-  for (int i0 = 0; i0 < 64; i0 += NIF) {
-    unsigned char fv[NIF];
-    float yv[NIF];
+  // Each wave scans its RPW rays one at a time, lane j on sample j (coalesced flag / value
+  // loads — all RPW rays' in flight at once — and ballots): refined = the flagged samples in
+  // front of the first unflagged sample that is certainly full, or up to and including it when
+  // it is an audited full sample (flag 3); every flag is cleared.  Flags 2/3 (audit, lite_flag)
+  // ride along in bit 30 of the candidate's index so the exact pass can check their class.
+  {
+    unsigned char fv[RPW];
+    float yv[RPW];
 #pragma unroll
-    for (int u = 0; u < NIF; ++u) {
-      const int rr = ch.ray0 + 64 * wv + i0 + u;
+    for (int u = 0; u < RPW; ++u) {
+      const int rr = ch.ray0 + RPW * wv + u;
       const bool in = rr < d.n_rays && lane < M;
       const size_t e = d.cand_off + (size_t)rr * M + lane;
       fv[u] = in ? refine[e] : 0;
       yv[u] = (in && dense) ? dense[e] : __builtin_nanf("");
     }
 #pragma unroll
-    for (int u = 0; u < NIF; ++u) {
-      const int rr = ch.ray0 + 64 * wv + i0 + u;
+    for (int u = 0; u < RPW; ++u) {
+      const int rr = ch.ray0 + RPW * wv + u;
       const uint64_t fb = __ballot(fv[u] != 0);
       const uint64_t ub = __ballot((fv[u] == 0 || fv[u] == 3) && yv[u] <= full);
       const uint64_t tb = __ballot(fv[u] == 3), ab = __ballot(fv[u] >= 2);
@@ -723,29 +724,36 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_refine_scan(const RenderChunk* 
         refine[d.cand_off + (size_t)rr * M + lane] = 0;
         if (slotmap) slotmap[d.cand_off + (size_t)rr * M + lane] = -1;   // k_refine_emit sets the refined
       }
-      if (lane == i0 + u) {
-        rbits[tid] = b;
-        abits[tid] = b & ab;
+      if (lane == u) {
+        rbits[RPW * wv + u] = b;
+        abits[RPW * wv + u] = b & ab;
       }
     }
   }
-  const uint64_t bits = rbits[tid], aud = abits[tid];
-  const int ray = ch.ray0 + tid;
-  if (ray < d.n_rays) {
-    rbits_g[d.ray_off + ray] = bits;
-    abits_g[d.ray_off + ray] = aud;
+  __syncthreads();
+  int cnt = 0, n_audit = 0;
+  if (tid < RENDER_RAYS) {
+    const uint64_t bits = rbits[tid], aud = abits[tid];
+    const int ray = ch.ray0 + tid;
+    if (ray < d.n_rays) {
+      rbits_g[d.ray_off + ray] = bits;
+      abits_g[d.ray_off + ray] = aud;
+    }
+    cnt = __popcll(bits);
+    n_audit = __popcll(aud);
   }
-  const int n_audit = __popcll(aud);
-  if (n_audit) atomicAdd(&S.n_audit, n_audit);
-  int cnt = __popcll(bits);
 #pragma unroll
-  for (int k = 32; k > 0; k >>= 1) cnt += __shfl_xor(cnt, k);
-  if (lane == 0) wsum[wv] = cnt;
+  for (int k = 32; k > 0; k >>= 1) {
+    cnt += __shfl_xor(cnt, k);
+    n_audit += __shfl_xor(n_audit, k);
+  }
+  if (lane == 0) { wsum[0][wv] = cnt; wsum[1][wv] = n_audit; }
   __syncthreads();
   if (tid == 0) {
-    int t = 0;
-    for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
+    int t = 0, a = 0;
+    for (int k = 0; k < NW; ++k) { t += wsum[0][k]; a += wsum[1][k]; }
     ccnt[blockIdx.x] = t;
+    if (a) atomicAdd(&S.n_audit, a);           // one atomic per chunk
   }
 }
 
