@@ -1976,6 +1976,7 @@ extern "C" int dsr_gather_layout(int n_obj, const dsr_object_in* in, int num_dep
   return 0;
 }
 
+extern "C++" {   // (inside the file's extern "C" block: C++ linkage for the helpers)
 namespace {
 // RCCL entry points, resolved from librccl at first use (no link-time dependency: a host
 // without RCCL still loads libdsr and gathers through host memory)
@@ -2031,6 +2032,7 @@ const std::vector<ncclComm_t>* comms_for(const std::vector<int>& devs, std::stri
   return &it->second;
 }
 }  // namespace
+}  // extern "C++"
 
 extern "C" int dsr_reconstruct_multi_ex(dsr_ctx* const* ctxs, const dsr_decoder* const* decs, int n_dev,
                                         const dsr_optim_params* p, int n_obj, const dsr_object_in* in,

@@ -354,6 +354,40 @@ def test_chunked_scan_with_four_groups_decodes_the_same_samples_every_run(gpu_de
                 assert np.array_equal(tr[i][key], ref_tr[i][key]), (run, i, key)
 
 
+def test_chunked_render_passes_match_the_per_object_pass_on_ragged_rays(gpu_decoder, monkeypatch):
+    """The render passes over ray chunks (k_sample_scan / k_sample_count + k_sample_emit, one
+    group) against the one-workgroup-per-object k_sample_pass (DSR_PRESCAN=0) on objects whose ray
+    counts straddle the 128-ray chunks — none, one, a few, 127 / 128 / 129, a partial last chunk,
+    a full KITTI object: bitwise equal results and per-iteration decoded / refined counts,
+    N_valid, K, H, b.  The ray-less object fails in its first iteration with loss 0 (no in-ball
+    samples: loss.py:86-88, optimizer.py:119, 144-145) — in k_iter_begin on the chunked path,
+    which has no workgroup for it."""
+    monkeypatch.setenv("DSR_TEST_HOOKS", "1")
+    monkeypatch.setenv("DSR_STREAMS", "1")
+    monkeypatch.delenv("DSR_RENDER_PASSES", raising=False)
+    opt = _opt(gpu_decoder, dict(S.KITTI_OPTIM, joint_optim=dict(S.KITTI_OPTIM["joint_optim"], num_iterations=3)),
+               "KITTI")
+    objs = []
+    for i, nr in enumerate((0, 1, 5, 127, 128, 129, 300, 2248)):
+        o = S.kitti_object(20 + i)
+        rays = np.ascontiguousarray(o.rays[:nr])
+        objs.append((o.t_cam_obj, o.pts, rays, np.ascontiguousarray(o.depth[:min(nr, o.depth.shape[0])]), None))
+    runs = {}
+    for pre in ("1", "0"):
+        monkeypatch.setenv("DSR_PRESCAN", pre)
+        runs[pre] = opt.reconstruct_objects(objs, trace=True)
+    (ra, ta), (rb, tb) = runs["1"], runs["0"]
+    for i in range(len(objs)):
+        a, b = ra[i], rb[i]
+        assert a["is_good"] == b["is_good"] and a["loss"] == b["loss"], i
+        if a["is_good"]:
+            assert np.array_equal(a["t_cam_obj"], b["t_cam_obj"]) and np.array_equal(a["code"], b["code"]), i
+        for key in ("H", "b", "n_valid", "k", "n_decoded", "n_refined"):
+            assert np.array_equal(ta[i][key], tb[i][key]), (i, key)
+    assert not ra[0]["is_good"] and ra[0]["loss"] == 0.0, ra[0]
+    assert ra[7]["is_good"] and ta[7]["n_decoded"].min() > 0 and ta[7]["n_refined"].min() > 0
+
+
 def test_failure_cases(gpu_decoder):
     f = golden("f6_fail.npz")
     opt = _opt(gpu_decoder, S.REDWOOD_OPTIM, "Redwood")
