@@ -1714,15 +1714,16 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
       ert.st = b->lite ? st : nullptr;
       ert.refine = b->refine;
       ert.diag = b->diag;
-      DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
-                                       (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       const bool chunked = b->prescan && gr.n_rch > 0;
+      if (!chunked)                              // (the chunked first pass fills its own rows)
+        DSR_CHECK(ctx, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b->dense + gr.c0), 0x7fc00000,
+                                         (size_t)(gr.c1 - gr.c0), s));   // out-of-ball samples: NaN
       for (int pz = 0; pz < np; ++pz) {          // render passes with early ray termination
         const int ra = b->passes[pz], rb = b->passes[pz + 1];
         if (chunked) {                           // count (the first pass: the ray scan), then emit
           if (pz == 0)
             hipLaunchKernelGGL(k_sample_scan, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                               b->M, rb, b->dead, b->rinfo, b->rwin, gr.scnt);
+                               b->M, rb, b->dead, b->rinfo, b->rwin, gr.scnt, b->dense);
           else
             hipLaunchKernelGGL(k_sample_count, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
                                b->M, ra, rb, b->dead, b->rinfo, b->rwin, gr.scnt);

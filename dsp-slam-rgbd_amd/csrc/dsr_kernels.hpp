@@ -405,13 +405,20 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_scan(const
                                                              const ObjState* __restrict__ st,
                                                              const float* __restrict__ rays_all, int M, int rb,
                                                              int* __restrict__ dead, int* __restrict__ rinfo,
-                                                             int* __restrict__ rwin, int* __restrict__ sc) {
+                                                             int* __restrict__ rwin, int* __restrict__ sc,
+                                                             float* __restrict__ dense) {
   const RenderChunk ch = chunks[blockIdx.x];
   const ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
   const ObjDesc d = desc[ch.obj];
   __shared__ SampleLds L;
   stage_samples(L, S, M, threadIdx.x);
+  {   // the chunk's rows of the sample values: NaN = out of the ball (loss.py:82; the passes'
+      // decodes overwrite the in-ball samples they reach)
+    const int nr = max(0, min(RENDER_RAYS, d.n_rays - ch.ray0));
+    float* row = dense + d.cand_off + (size_t)ch.ray0 * M;
+    for (int e = threadIdx.x; e < nr * M; e += RENDER_RAYS) row[e] = __builtin_nanf("");
+  }
   __syncthreads();
 #ifdef DSR_EXP_PROV
   if (threadIdx.x == 0) prov_state(1, S.iters_done, d.ray_off + ch.ray0, prov_sum(L.T, L.depths, M));
