@@ -1048,30 +1048,41 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   if (tid < M) dep_s[tid] = S.depths[tid];
   const int nr = min(RENDER_RAYS, d.n_rays - ch.ray0);
   {
-    // element e -> (row e / M, column e % M) advanced without per-element divisions; 16
-    // loads in flight per thread before their LDS stores (a chunk's 128 x M values in ~4
-    // rounds of load latency: the staging was most of this kernel's time with 4)
-    constexpr int NLD = 16;
+    // The chunk's rows are one contiguous run of nr * M floats: read as 16-byte loads (a scalar
+    // head up to the first aligned address, a scalar tail), all of a thread's loads in flight
+    // before its LDS stores — one round of load latency (4-byte loads, 16 in flight, took 4)
     const float* src = dense + d.cand_off + (size_t)ch.ray0 * M;
-    const int tot = nr * M, sq = RENDER_RAYS / M, sr = RENDER_RAYS - sq * M;
-    int r = tid / M, j = tid - r * M;
-    for (int e = tid; e < tot; e += NLD * RENDER_RAYS) {
-      float v[NLD];
-      int o[NLD];
+    const int tot = nr * M;
+    const int head = min(tot, (int)(((16 - ((uintptr_t)src & 15)) & 15) >> 2));
+    const int n4 = (tot - head) >> 2, tail0 = head + 4 * n4;
+    auto put = [&](int e, float v) {
+      const int r = e / M, j = e - r * M;
+      T_s[r * pitch + j] = v;
+      D_s[r * pitch + j] = v;
+    };
+    constexpr int NV = (MAXM * RENDER_RAYS / 4 + RENDER_RAYS - 1) / RENDER_RAYS;
+    const float4* s4 = reinterpret_cast<const float4*>(src + head);
+    float4 v[NV];
 #pragma unroll
-      for (int u = 0; u < NLD; ++u) {
-        v[u] = (e + u * RENDER_RAYS < tot) ? src[e + u * RENDER_RAYS] : 0.f;
-        o[u] = r * pitch + j;
-        j += sr;
-        r += sq;
-        if (j >= M) { j -= M; ++r; }
-      }
+    for (int u = 0; u < NV; ++u) {
+      const int i = tid + u * RENDER_RAYS;
+      v[u] = i < n4 ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < head) put(tid, src[tid]);
+    if (tid < tot - tail0) put(tail0 + tid, src[tail0 + tid]);
 #pragma unroll
-      for (int u = 0; u < NLD; ++u)
-        if (e + u * RENDER_RAYS < tot) {
-          T_s[o[u]] = v[u];
-          D_s[o[u]] = v[u];
+    for (int u = 0; u < NV; ++u) {
+      const int i = tid + u * RENDER_RAYS;
+      if (i < n4) {
+        const int e = head + 4 * i;
+        int r = e / M, j = e - r * M;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          T_s[r * pitch + j] = fetch4(v[u], k);
+          D_s[r * pitch + j] = fetch4(v[u], k);
+          if (++j == M) { j = 0; ++r; }
         }
+      }
     }
   }
   __syncthreads();
@@ -2115,80 +2126,88 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k), hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
   };
-  // Blocked right-looking Cholesky, panels of CPW columns: wave 0 factors a panel in registers
-  // (lane l holds rows c0 + l and c0 + 64 + l; the pivot value and the panel's L[c'][c] reach the
-  // other lanes by v_readlane), then all waves apply the panel to the trailing triangle (rows and
-  // columns >= c1, the b row included) — 2 barriers per panel instead of 1 per column.
+  // Blocked right-looking Cholesky with look-ahead, panels of CPW columns.  Wave 0 factors a panel
+  // in registers (lane l holds rows c0 + l and c0 + 64 + l; the pivot value and the panel's
+  // L[c'][c] reach the other lanes by v_readlane) after applying the previous panel to the
+  // panel's own columns itself; meanwhile waves 1-4 apply the previous panel to the rest of the
+  // trailing triangle (columns past the new panel, the b row included): one barrier per panel.
+  // Every element still takes the panels' updates in panel order, each as the same 8 products
+  // subtracted in the same order, so the factors are bitwise those of panel-then-update steps.
   constexpr int CPW = 8;
-#ifdef DSR_SOLVE_PROFILE
-  long long t_pan = 0, t_upd = 0;
-#endif
-  for (int c0 = 0; c0 < NPAR; c0 += CPW) {
-    const int c1 = min(c0 + CPW, NPAR);
-#ifdef DSR_SOLVE_PROFILE
-    const long long tq0 = wall_clock64();
-#endif
-    if (tid < 64) {
-      // the panel's W columns with W a compile-time width (CPW, or NPAR % CPW for the last
-      // panel): straight-line code, no per-column guards
-      auto panel = [&](auto WC) {
-        constexpr int W = decltype(WC)::value;
-        const int r0 = c0 + tid, r1 = r0 + 64;
-        double a0[W], a1[W];
+  static_assert(NPAR % CPW == 7, "last panel width");
+  // wave 0: columns [c0, c0 + W) of rows c0..NPAR, first updated by panel [pc, pc + CPW) if pc >= 0
+  auto panel = [&](auto WC, int c0, int pc) {
+    constexpr int W = decltype(WC)::value;
+    const int r0 = c0 + tid, r1 = r0 + 64;
+    double a0[W], a1[W];
 #pragma unroll
-        for (int u = 0; u < W; ++u) {
-          a0[u] = (r0 <= NPAR && c0 + u <= r0) ? Lc[r0][c0 + u] : 0.0;
-          a1[u] = r1 <= NPAR ? Lc[r1][c0 + u] : 0.0;
-        }
-        bool bad = false;
-#pragma unroll
-        for (int u = 0; u < W; ++u) {
-          const double d2 = bcastk(a0[u], u);                   // row c0 + u sits in lane u
-          bad = bad || !(d2 > 0.0);
-          // 1/sqrt(d2): an fp32 seed (v_rsq_f32, 1 ulp) and two Newton steps in fp64
-          double rs = (double)__builtin_amdgcn_rsqf((float)d2);
-          const double hd = 0.5 * d2;
-          rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
-          rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
-          a0[u] = (tid == u) ? d2 * rs : a0[u] * rs;
-          a1[u] = a1[u] * rs;
-          if (tid == 0) rdg[c0 + u] = rs;
-#pragma unroll
-          for (int w = u + 1; w < W; ++w) {                     // the panel's later columns
-            const double lwu = bcastk(a0[u], w);                // L[c0 + w][c0 + u]
-            a0[w] -= a0[u] * lwu;
-            a1[w] -= a1[u] * lwu;
-          }
-        }
-        if (tid == 0 && bad) chol_bad = 1;
-#pragma unroll
-        for (int u = 0; u < W; ++u) {
-          if (r0 <= NPAR && c0 + u <= r0) Lc[r0][c0 + u] = a0[u];
-          if (r1 <= NPAR) Lc[r1][c0 + u] = a1[u];
-        }
-      };
-      static_assert(NPAR % CPW == 7, "last panel width");
-      if (c1 - c0 == CPW) panel(std::integral_constant<int, CPW>{});
-      else panel(std::integral_constant<int, NPAR % CPW>{});
+    for (int u = 0; u < W; ++u) {
+      a0[u] = (r0 <= NPAR && c0 + u <= r0) ? Lc[r0][c0 + u] : 0.0;
+      a1[u] = r1 <= NPAR ? Lc[r1][c0 + u] : 0.0;
     }
-    __syncthreads();
-#ifdef DSR_SOLVE_PROFILE
-    const long long tq1 = wall_clock64();
-    t_pan += tq1 - tq0;
-#endif
-    // trailing update by the panel: A[i][j] -= sum_u L[i][c0+u] L[j][c0+u], c1 <= j <= i, j < NPAR,
-    // in 4 x 4 element blocks (block row bi >= block column bj), one per thread: the 8 panel values
-    // of its 4 rows and 4 columns are loaded once (16-byte reads) and reused across the block
-    {
-      // (after the last panel, c1 = NPAR, nothing is left: every other panel is CPW wide)
-      const int nr = NPAR + 1 - c1, nb = (nr + 3) >> 2;
-      const int t = tid;
-      if (c1 < NPAR && t < nb * (nb + 1) / 2) {
+    if (pc >= 0) {              // (rows above the diagonal get garbage here: never stored)
+      double p0[CPW], p1[CPW];  // this lane's rows of the previous panel
+#pragma unroll
+      for (int v = 0; v < CPW; ++v) {
+        p0[v] = r0 <= NPAR ? Lc[r0][pc + v] : 0.0;
+        p1[v] = r1 <= NPAR ? Lc[r1][pc + v] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < W; ++u)
+#pragma unroll
+        for (int v = 0; v < CPW; ++v) {
+          const double lw = Lc[c0 + u][pc + v];
+          a0[u] -= p0[v] * lw;
+          a1[u] -= p1[v] * lw;
+        }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      const double d2 = bcastk(a0[u], u);                   // row c0 + u sits in lane u
+      bad = bad || !(d2 > 0.0);
+      // 1/sqrt(d2): an fp32 seed (v_rsq_f32, 1 ulp) and two Newton steps in fp64
+      double rs = (double)__builtin_amdgcn_rsqf((float)d2);
+      const double hd = 0.5 * d2;
+      rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
+      rs = rs * __builtin_fma(-hd * rs, rs, 1.5);
+      a0[u] = (tid == u) ? d2 * rs : a0[u] * rs;
+      a1[u] = a1[u] * rs;
+      if (tid == 0) rdg[c0 + u] = rs;
+#pragma unroll
+      for (int w = u + 1; w < W; ++w) {                     // the panel's later columns
+        const double lwu = bcastk(a0[u], w);                // L[c0 + w][c0 + u]
+        a0[w] -= a0[u] * lwu;
+        a1[w] -= a1[u] * lwu;
+      }
+    }
+    if (tid == 0 && bad) chol_bad = 1;
+#pragma unroll
+    for (int u = 0; u < W; ++u) {
+      if (r0 <= NPAR && c0 + u <= r0) Lc[r0][c0 + u] = a0[u];
+      if (r1 <= NPAR) Lc[r1][c0 + u] = a1[u];
+    }
+  };
+  if (tid < 64) panel(std::integral_constant<int, CPW>{}, 0, -1);
+  __syncthreads();
+  for (int c0 = 0; c0 + CPW < NPAR; c0 += CPW) {    // panel [c0, c1) is factored
+    const int c1 = c0 + CPW, c2 = min(c1 + CPW, NPAR);
+    if (tid < 64) {
+      if (c2 - c1 == CPW) panel(std::integral_constant<int, CPW>{}, c1, c0);
+      else panel(std::integral_constant<int, NPAR % CPW>{}, c1, c0);
+    } else if (c2 < NPAR) {
+      // trailing update by panel [c0, c1): A[i][j] -= sum_u L[i][c0+u] L[j][c0+u], c2 <= j <= i,
+      // j < NPAR, in 4 x 4 element blocks (block row bi >= block column bj), one per thread of
+      // waves 1-4: the 8 panel values of its 4 rows and 4 columns are loaded once (16-byte
+      // reads) and reused across the block
+      const int nr = NPAR + 1 - c2, nb = (nr + 3) >> 2;
+      const int t = tid - 64;
+      if (t < nb * (nb + 1) / 2) {
         int bi = (int)((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
         while (bi * (bi + 1) / 2 > t) --bi;
         while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
         const int bj = t - bi * (bi + 1) / 2;
-        const int i0 = c1 + 4 * bi, j0 = c1 + 4 * bj;
+        const int i0 = c2 + 4 * bi, j0 = c2 + 4 * bj;
         double li[4][CPW], lj[4][CPW];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -2229,9 +2248,6 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
       }
     }
     __syncthreads();
-#ifdef DSR_SOLVE_PROFILE
-    t_upd += wall_clock64() - tq1;
-#endif
   }
 #ifdef DSR_SOLVE_PROFILE
   const long long tp2 = wall_clock64();
@@ -2395,7 +2411,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   }
 #ifdef DSR_SOLVE_PROFILE                 // (tools: per-phase wall clock of block 0, 100 MHz ticks)
   const long long tp3 = wall_clock64();
-  if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2, t_pan, t_upd);
+  if (tid == 0 && o == 0) printf("solve_prof %lld %lld %lld\n", tp1 - tp0, tp2 - tp1, tp3 - tp2);
 #endif
   if (tid < CODE) zbuf[o * CODE + tid] = z[tid] + P.lr * dx[NPOSE + tid];   // :194
   if (tid == 0) {
