@@ -2115,7 +2115,7 @@ __global__ __launch_bounds__(SOLVE_THREADS) void k_solve(int n_obj, const ObjDes
   // H = L L^T in fp64, with b carried as an extra row of L (row NPAR: the forward substitution
   // L y = b rides along in the factorisation) and one back substitution L^T dx = y: no pivot
   // search, no row swaps, two barriers per 8-column panel (the LU + explicit
-  // inverse it replaces took 63 + 21 us per solve, this 25 + 6.5).  dx is at least as accurate as the reference's fp32
+  // inverse it replaces took 63 + 21 us per solve, this 13.6 + 3.6).  dx is at least as accurate as the reference's fp32
   // inverse-times-b (tests/test_gpu_parity.py::test_teacher_forced_steps_no_less_accurate_than_
   // the_reference holds it against fp64 truth).  A non-positive or NaN pivot (an H with NaN or
   // inf entries) falls back to the fp32 LU with partial pivoting below, the reference's own
