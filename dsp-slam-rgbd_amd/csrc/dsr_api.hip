@@ -1273,11 +1273,14 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
   }
 #endif
   {
-    // The first pass's ray scan as its own chunked launch (k_sample_scan) for one-group batches
-    // — single calls, graph-mode keyframe slots — where it takes ~0.3 ms off a KITTI object's call.
-    // Its round-4/5 timing-dependent decode counts were wrong products of a packed-FP32 multiply
-    // in its loop's first trip; the kernel is built without packed FP32 now.
-    // DSR_PRESCAN=0/1 (test hook) forces it.
+    // The render passes over the ray chunks (a count kernel — k_sample_scan for the first pass,
+    // k_sample_count after — then k_sample_emit) for one-group batches: single calls, graph-mode
+    // keyframe slots, where one object's pass otherwise runs on one workgroup (DESIGN.md §3.8:
+    // a KITTI call 8.8 -> 7.9 ms with the chunked first-pass scan alone, -0.4 ms more with every
+    // pass chunked).  Multi-group batches measured equal either way and keep k_sample_pass.  The
+    // scan's round-4/5 timing-dependent decode counts were wrong products of a packed-FP32
+    // multiply in its loop's first trip (§3.9); these kernels are built without packed FP32.
+    // DSR_PRESCAN=0/1 (test hook) forces one form.
     const char* e = hook_env("DSR_PRESCAN");
     b->prescan = e ? atoi(e) != 0 : b->groups.size() == 1;
   }

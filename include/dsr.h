@@ -186,8 +186,9 @@ typedef struct {
                                      _LITE_VARIANT / _SPLIT_RING move these from the shipped values.
                                      ABI 11: the four are the kernels the last run DISPATCHED
                                      (recorded as it was enqueued), not the environment's values */
-  int prescan;                    /* ABI 11: 1 if the first render pass's ray scan ran as its own
-                                     chunked launch (k_sample_scan; one-group batches) */
+  int prescan;                    /* ABI 11: 1 if the render passes ran over the ray chunks
+                                     (k_sample_scan / k_sample_count + k_sample_emit; one-group
+                                     batches), 0 for one workgroup per object (k_sample_pass) */
 } dsr_stats;
 
 /* ---- context ------------------------------------------------------------- */
