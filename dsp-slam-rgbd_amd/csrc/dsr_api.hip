@@ -1276,8 +1276,9 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     // The render passes over the ray chunks (a count kernel — k_sample_scan for the first pass,
     // k_sample_count after — then k_sample_emit) for one-group batches: single calls, graph-mode
     // keyframe slots, where one object's pass otherwise runs on one workgroup (DESIGN.md §3.8:
-    // a KITTI call 8.8 -> 7.9 ms with the chunked first-pass scan alone, -0.4 ms more with every
-    // pass chunked).  Multi-group batches measured equal either way and keep k_sample_pass.  The
+    // a KITTI call 8.77 -> 8.14 ms with the chunked first-pass scan alone, Appendix A D1; every
+    // pass chunked, with the render staging of the same change, 7.50 -> 7.05 ms, r6y).
+    // Multi-group batches measured equal either way and keep k_sample_pass.  The
     // scan's round-4/5 timing-dependent decode counts were wrong products of a packed-FP32
     // multiply in its loop's first trip (§3.9); these kernels are built without packed FP32.
     // DSR_PRESCAN=0/1 (test hook) forces one form.
