@@ -1009,17 +1009,26 @@ def test_ray_chunk_boundaries_vs_oracle(gpu_decoder, oracle_dec):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("m", [17, 32, 64])
-def test_depth_sample_counts_vs_oracle(gpu_decoder, oracle_dec, m):
+def test_depth_sample_counts_vs_oracle(gpu_decoder, oracle_dec, m, monkeypatch):
     """num_depth_samples (configs' `num_depth_samples`, optimizer.py:126) other than 50:
     odd, small, and the largest supported (64: every lane of the refine scan, the largest
-    render LDS rows) — the first GN step of a small batch vs the oracle's."""
+    render LDS rows) — the first GN step of a small batch vs the oracle's; and the same batch
+    as one object group (the render passes over ray chunks, rows of M samples at any 4-byte
+    alignment in the render staging) bitwise equal to the default grouping."""
     from oracle import dsr_oracle as O
 
     optim = dict(S.REDWOOD_OPTIM, num_depth_samples=m,
                  joint_optim=dict(S.REDWOOD_OPTIM["joint_optim"], num_iterations=1))
     opt = _opt(gpu_decoder, optim, "Redwood")
     obs = [S.redwood_object(60 + i, n_pts=300) for i in range(3)]
-    res, tr = opt.reconstruct_objects([(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in obs], trace=True)
+    objs = [(o.t_cam_obj, o.pts, o.rays, o.depth, None) for o in obs]
+    res, tr = opt.reconstruct_objects(objs, trace=True)
+    monkeypatch.setenv("DSR_STREAMS", "1")
+    res1, tr1 = opt.reconstruct_objects(objs, trace=True)
+    for i in range(len(objs)):
+        assert res1[i]["loss"] == res[i]["loss"], (m, i)
+        for key in ("H", "b", "n_valid", "k", "n_decoded", "n_refined"):
+            assert np.array_equal(tr1[i][key], tr[i][key]), (m, i, key)
     P = O.OptimParams.from_cfg(optim)
     assert P.num_depth_samples == m
     for i, o in enumerate(obs):
