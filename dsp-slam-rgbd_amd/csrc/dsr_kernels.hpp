@@ -382,6 +382,24 @@ __device__ __forceinline__ void chunk_sums(int a, int b, int* __restrict__ out) 
   }
 }
 
+// v[stride * c] summed over chunks c in [c0, c1) by the whole block (call it uniformly): the
+// loads in parallel, one latency, where a serial walk over an object's earlier chunks waited
+// once per chunk (up to ~1 us each, ~18 chunks for a KITTI object).  Integer sums: any order.
+__device__ __forceinline__ int block_chunk_sum(const int* __restrict__ v, int stride, int c0, int c1) {
+  __shared__ int ws[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  int x = 0;
+  for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) x += v[(size_t)stride * c];
+#pragma unroll
+  for (int k = 32; k > 0; k >>= 1) x += __shfl_xor(x, k);
+  if (lane == 0) ws[wv] = x;
+  __syncthreads();
+  int t = 0;
+  for (int k = 0; k < nw; ++k) t += ws[k];
+  __syncthreads();                       // (ws reusable by the next call)
+  return t;
+}
+
 // The in-ball samples of ranks [ra, rb) of a ray whose in-ball set is not one run (rank =
 // position among the ray's in-ball samples, depth order): their number, and the ray's in-ball
 // total when the walk is not cut at rb.
@@ -511,8 +529,9 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_emit(const
   __shared__ SampleLds L;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   stage_samples(L, S, M, tid);
-  int base = 0;
-  for (int c = ch.first; c < (int)blockIdx.x; ++c) base += sc[2 * c];
+  const bool last = (int)blockIdx.x == ch.first + ch.n - 1;   // the object's last chunk: its totals
+  const int base = block_chunk_sum(sc, 2, ch.first, blockIdx.x);
+  const int nin = (last && ra == 0) ? block_chunk_sum(sc + 1, 2, ch.first, blockIdx.x + 1) : 0;
   const int ray = ch.ray0 + tid;
   int cnt = 0, j0 = -1;
   float3 rv = make_float3(0.f, 0.f, 0.f);
@@ -545,14 +564,12 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_emit(const
       ++rank;
     }
   }
-  if (tid == 0 && (int)blockIdx.x == ch.first + ch.n - 1) {   // the object's last chunk: its totals
+  if (tid == 0 && last) {
     int t = base;
     for (int k = 0; k < RENDER_RAYS / 64; ++k) t += wsum[k];
     S.n_emit = t;
     S.n_eval += t;
     if (ra == 0) {
-      int nin = 0;
-      for (int c = ch.first; c <= (int)blockIdx.x; ++c) nin += sc[2 * c + 1];
       S.n_valid = nin;
       if (nin < 10) {                          // loss.py:86-88 -> optimizer.py:144-145
         S.status = ST_FAIL;
@@ -779,8 +796,7 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_refine_emit(const
   __shared__ SampleLds L;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   stage_samples(L, S, M, tid);
-  int base = 0;
-  for (int c = ch.first; c < (int)blockIdx.x; ++c) base += ccnt[c];
+  const int base = block_chunk_sum(ccnt, 1, ch.first, blockIdx.x);
   const int ray = ch.ray0 + tid;
   uint64_t bits = 0, aud = 0;
   float3 rv = make_float3(0.f, 0.f, 0.f);
@@ -1170,8 +1186,7 @@ __global__ __launch_bounds__(256) void k_render_gather(const RenderChunk* __rest
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
   const ObjDesc d = desc[ch.obj];
-  int off = 0;
-  for (int c = ch.first; c < (int)blockIdx.x; ++c) off += ccnt[c];
+  const int off = block_chunk_sum(ccnt, 1, ch.first, blockIdx.x);
   const int n = ccnt[blockIdx.x];
   if (threadIdx.x == 0 && (int)blockIdx.x == ch.first + ch.n - 1) S.k = off + n;
   const size_t s0 = (size_t)d.cand_off + (size_t)ch.ray0 * M, d0 = (size_t)d.cand_off + off;
