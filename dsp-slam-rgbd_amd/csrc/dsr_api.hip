@@ -274,6 +274,7 @@ struct dsr_batch {
     RenderChunk* rchunks = nullptr;   // k_render_rays chunks of the group's objects
     int* ccnt = nullptr;              // render points per chunk
     int* scnt = nullptr;              // chunked render passes: samples, in-ball samples per chunk
+    int2* och = nullptr;              // per object: first chunk, chunks (the chunked path's tile tables)
     int n_rch = 0;
   };
   std::vector<Group> groups;
@@ -1336,16 +1337,20 @@ static int batch_create_impl(dsr_ctx* ctx, const dsr_decoder* dec, const dsr_opt
     ALLOC(gr.nt_j, sizeof(int));
     ALLOC(gr.sync, 8 * 32 * sizeof(unsigned));
     std::vector<RenderChunk> rch;
+    std::vector<int2> och;
     for (int o = gr.o0; o < gr.o0 + gr.n; ++o) {
       const int first = (int)rch.size(), nch = (b->hdesc[o].n_rays + RENDER_RAYS - 1) / RENDER_RAYS;
       for (int c = 0; c < nch; ++c) rch.push_back(RenderChunk{o - gr.o0, c * RENDER_RAYS, first, nch});
+      och.push_back(make_int2(first, nch));
     }
     gr.n_rch = (int)rch.size();
     ALLOC(gr.rchunks, sizeof(RenderChunk) * rch.size());
     ALLOC(gr.ccnt, sizeof(int) * rch.size());
     ALLOC(gr.scnt, 2 * sizeof(int) * rch.size());
+    ALLOC(gr.och, sizeof(int2) * och.size());
     if (!rch.empty() &&
-        hipMemcpy(gr.rchunks, rch.data(), sizeof(RenderChunk) * rch.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (hipMemcpy(gr.rchunks, rch.data(), sizeof(RenderChunk) * rch.size(), hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(gr.och, och.data(), sizeof(int2) * och.size(), hipMemcpyHostToDevice) != hipSuccess)) {
       dsr_batch_destroy(b);
       return fail(ctx, "hipMemcpy (render chunks) failed");
     }
@@ -1731,14 +1736,16 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
           else
             hipLaunchKernelGGL(k_sample_count, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
                                b->M, ra, rb, b->dead, b->rinfo, b->rwin, gr.scnt);
-          hipLaunchKernelGGL(k_sample_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                             b->M, ra, rb, b->cand, b->rwin, gr.scnt);
+          // (+1 workgroup: the pass's tile table, from the count kernel's chunk counts)
+          hipLaunchKernelGGL(k_sample_emit, dim3(gr.n_rch + 1), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st,
+                             b->rays, b->M, ra, rb, b->cand, b->rwin, gr.scnt,
+                             ChunkTiles{gr.och, gr.tiles_f, gr.nt_f, ng, b->lite ? LTILE : TILE, 0});
         } else {
           hipLaunchKernelGGL(k_sample_pass, dim3(ng), dim3(SAMPLE_THREADS), 0, s, ng, desc, st, b->rays, b->M,
                              ra, rb, b->cand, b->dead, b->rinfo);
+          hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
+                             b->lite ? LTILE : TILE, 0);
         }
-        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f,
-                           b->lite ? LTILE : TILE, 0);
         if (fv & 1) DSR_CHECK(ctx, hipMemsetAsync(gr.sync, 0, 8 * 32 * sizeof(unsigned), s));
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * pz], s));
         if (b->lite)
@@ -1755,11 +1762,14 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
           hipLaunchKernelGGL(k_refine_scan, dim3(gr.n_rch), dim3(REFINE_SCAN_THREADS), 0, s, gr.rchunks, desc, st, b->M,
                              b->refine, refine_all() ? nullptr : b->dense, -P.cut_off, b->rbits, b->abits, gr.ccnt,
                              b->ma.slotmap);
-          hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch), dim3(RENDER_RAYS), 0, s, gr.rchunks, desc, st, b->rays,
-                             b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt);
+          const int wp = (b->ma.pts && fv == 12) ? 1 : 0;   // (chunked: +1 workgroup, the exact pass's tiles)
+          hipLaunchKernelGGL(k_refine_emit, dim3(gr.n_rch + (chunked ? 1 : 0)), dim3(RENDER_RAYS), 0, s, gr.rchunks,
+                             desc, st, b->rays, b->M, b->cand, b->ma.slotmap, b->rbits, b->abits, gr.ccnt,
+                             chunked ? ChunkTiles{gr.och, gr.tiles_f, gr.nt_f, ng, TILE, wp} : ChunkTiles{});
         }
-        hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
-                           (b->ma.pts && fv == 12) ? 1 : 0);
+        if (!chunked)
+          hipLaunchKernelGGL(k_tiles_fwd, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_f, gr.nt_f, TILE,
+                             (b->ma.pts && fv == 12) ? 1 : 0);
         if (timing) DSR_CHECK(ctx, hipEventRecord(ev[2 * np], s));
         const ErtArgs ex{nullptr, b->M, -P.cut_off, st, nullptr};
         if (b->ma.msk && fv == 12)               // keep masks + sdf for the Jacobian's render points
@@ -1776,10 +1786,13 @@ static int batch_enqueue_iters(dsr_batch* b, bool timing, int it0, int it1) {
         hipLaunchKernelGGL(k_render_rays, dim3(gr.n_rch), dim3(RENDER_RAYS), render_lds_bytes(b->M), s,
                            gr.rchunks, desc, st, b->rays, b->dobs, P, b->dense, b->kst, b->rst,
                            keep ? b->sst : nullptr, (const int*)b->ma.slotmap, gr.ccnt);
-        hipLaunchKernelGGL(k_render_gather, dim3(gr.n_rch), dim3(256), 0, s, gr.rchunks, desc, st, gr.ccnt, b->M,
-                           b->kst, b->rst, b->sst, b->kpts, b->kres, keep ? b->kslot : nullptr);
+        // (chunked: +1 workgroup, the Jacobian's tiles from the render chunks' counts)
+        hipLaunchKernelGGL(k_render_gather, dim3(gr.n_rch + (chunked ? 1 : 0)), dim3(256), 0, s, gr.rchunks, desc,
+                           st, gr.ccnt, b->M, b->kst, b->rst, b->sst, b->kpts, b->kres, keep ? b->kslot : nullptr,
+                           chunked ? ChunkTiles{gr.och, gr.tiles_j, gr.nt_j, ng, TILE, 0} : ChunkTiles{});
       }
-      hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
+      if (!chunked)
+        hipLaunchKernelGGL(k_tiles_jac, dim3(1), dim3(1024), 0, s, ng, desc, st, gr.tiles_j, gr.nt_j);
       if (timing) DSR_CHECK(ctx, hipEventRecord(ev[je], s));
       hipLaunchKernelGGL(jack, dim3(grid), dim3(512), 0, s, D, gr.tiles_j, gr.nt_j, desc, st,
                          b->pts, b->kpts, b->kres, b0, b4, P, b->slots,

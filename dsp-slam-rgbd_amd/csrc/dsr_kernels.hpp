@@ -350,6 +350,171 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// One object's chunk counts cnt[stride * c], c in [c0, c0 + n), by one thread, 8 loads in flight.
+__device__ __forceinline__ int object_chunk_sum(const int* __restrict__ cnt, int stride, int c0, int n) {
+  int t = 0;
+  for (int k = 0; k < n; k += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (k + u < n) ? cnt[(size_t)stride * (c0 + k + u)] : 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  return t;
+}
+
+// ------------------------------------------------------------------------------------
+// tile tables (single workgroup)
+// ------------------------------------------------------------------------------------
+// Tile tables (one block of 1024 threads): a block-wide exclusive scan of the per-object tile
+// counts gives every object its first tile; then the whole block writes the tiles, thread t
+// taking tiles t, t + 1024, ... of the chunk and finding its object by a binary search over
+// the chunk's first-tile offsets in LDS (one thread per object writing all of that object's
+// tiles was a serial loop of ~250 stores for one KITTI object's render pass, ~10 us).
+// Object order, then tile order within an object — the table the serial loop would build.
+constexpr int TILE_SCAN_THREADS = 1024;
+template <class Count, class Emit>
+__device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit emit) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  __shared__ int first_s[TILE_SCAN_THREADS + 1];   // chunk-relative first tile per object, + total
+  __shared__ int n_s[TILE_SCAN_THREADS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+  if (tid == 0) carry = base;
+  __syncthreads();
+  for (int o0 = 0; o0 < n_obj; o0 += blockDim.x) {
+    const int o = o0 + tid;
+    const int m = min((int)blockDim.x, n_obj - o0);   // objects in this chunk
+    int n = 0, nt = 0;
+    if (o < n_obj) count(o, n, nt);
+    const int inc = wave_incl_scan(nt, lane);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    if (wv == 0) {
+      int v = lane < nw ? wsum[lane] : 0;
+      v = wave_incl_scan(v, lane);
+      if (lane < nw) wsum[lane] = v;
+    }
+    __syncthreads();
+    if (tid < m) {
+      first_s[tid] = (wv ? wsum[wv - 1] : 0) + inc - nt;
+      n_s[tid] = n;
+    }
+    if (tid == 0) first_s[m] = wsum[nw - 1];
+    __syncthreads();
+    const int c0 = carry, ct = first_s[m];
+    for (int t = tid; t < ct; t += blockDim.x) {
+      int lo = 0, hi = m - 1;                 // last object whose first tile is <= t
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (first_s[mid] <= t) lo = mid; else hi = mid - 1;
+      }
+      emit(c0 + t, o0 + lo, t - first_s[lo], n_s[lo]);
+    }
+    __syncthreads();
+    if (tid == 0) carry += ct;
+    __syncthreads();
+  }
+  return carry;
+}
+
+// with_pts (exact pass, kept masks): each object's sample tiles, then its surface-point
+// tiles (term 3, the same 64-point groups as the Jacobian's sdf tiles).  `count(o)` gives an
+// object's samples, or -1 for an object that gets no tile.
+template <class Count>
+__device__ __forceinline__ void build_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, Count count,
+                                                Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize,
+                                                int with_pts) {
+  const int total = tile_scan(
+      n_obj, 0,
+      [&](int o, int& n, int& nt) {
+        const int c = count(o);
+        n = max(c, 0);
+        nt = (n + tsize - 1) / tsize;
+        if (with_pts && c >= 0) nt += (desc[o].n_pts + TILE - 1) / TILE;
+      },
+      [&](int idx, int o, int i, int n) {
+        Tile t;
+        const int nb = (n + tsize - 1) / tsize;
+        t.obj = o;
+        if (i < nb) {
+          t.term = 0; t.start = i * tsize;
+          t.count = min(tsize, n - i * tsize);
+        } else {
+          t.term = 3; t.start = (i - nb) * TILE;
+          t.count = min(TILE, desc[o].n_pts - t.start);
+        }
+        tiles[idx] = t;
+      });
+  if (threadIdx.x == 0) *n_tiles = total;
+}
+
+__global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize, int with_pts) {
+  build_tiles_fwd(
+      n_obj, desc, [&](int o) { return st[o].status == ST_RUNNING ? st[o].n_emit : -1; }, tiles, n_tiles,
+      tsize, with_pts);
+}
+
+// Every object's sdf tiles (forward + backward) first, then every render tile (backward
+// only, kept masks): the persistent grid's blocks then run tiles of one kind together, so
+// the layers they stream stay in step (L2-resident weights).  Tile outputs go to slots
+// derived from the tile itself (jac_tail), so the order changes no result.  `k_of(o)`: the
+// object's render points K.
+template <class KOf>
+__device__ __forceinline__ void build_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st, KOf k_of,
+                                                Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+  int total = 0;
+  for (int term = 0; term < 2; ++term)
+    total = tile_scan(
+        n_obj, total,
+        [&](int o, int& n, int& nt) {
+          ObjState& S = st[o];
+          n = (S.status == ST_RUNNING) ? (term == 0 ? desc[o].n_pts : k_of(o)) : 0;
+          nt = (n + TILE - 1) / TILE;
+          if (term == 0) S.n_sdf_tiles = nt;
+          else S.n_ren_tiles = nt;
+        },
+        [&](int idx, int o, int i, int n) {
+          Tile t;
+          t.obj = o; t.term = term; t.start = i * TILE;
+          t.count = min(TILE, n - i * TILE);
+          tiles[idx] = t;
+        });
+  if (threadIdx.x == 0) *n_tiles = total;
+}
+
+__global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
+                            Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
+  build_tiles_jac(n_obj, desc, st, [&](int o) { return st[o].k; }, tiles, n_tiles);
+}
+
+// The same tables built by one extra workgroup of the emit / gather kernels of the chunked
+// (one-group) path, from the per-chunk counts the previous launch left — the counts the
+// emitting workgroups turn into S.n_emit / S.n_refine / S.k meanwhile — so no workgroup waits
+// on another and the separate table launch (~4 us + its gap) goes.  `och[o]` = the object's
+// first chunk and chunk count.  First pass: an object with fewer than 10 in-ball samples gets
+// no tile (the emitting workgroups fail it, loss.py:86-88), as k_tiles_fwd would see it.
+struct ChunkTiles {
+  const int2* och;   // nullptr: no extra workgroup (the kernel's grid is the chunks)
+  Tile* tiles;
+  int* n_tiles;
+  int n_obj, tsize, with_pts;
+};
+__device__ __forceinline__ void chunk_tiles_fwd(const ChunkTiles& T, const ObjDesc* __restrict__ desc,
+                                                const ObjState* __restrict__ st, const int* __restrict__ cnt,
+                                                int stride, const int* __restrict__ nin) {
+  build_tiles_fwd(
+      T.n_obj, desc,
+      [&](int o) {
+        const int2 oc = T.och[o];
+        if (st[o].status != ST_RUNNING) return -1;
+        if (nin && object_chunk_sum(nin, stride, oc.x, oc.y) < 10) return -1;
+        return object_chunk_sum(cnt, stride, oc.x, oc.y);
+      },
+      T.tiles, T.n_tiles, T.tsize, T.with_pts);
+}
+
 // Chunked render passes (one thread per ray, one workgroup per RENDER_RAYS rays of an object,
 // the render chunk table): a pass is a count kernel — k_sample_scan for the first pass, which
 // also records each ray's in-ball run (loss.py:82) and clears its dead flag, k_sample_count for
@@ -520,7 +685,11 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_emit(const
                                                              const float* __restrict__ rays_all, int M, int ra,
                                                              int rb, float4* __restrict__ cand,
                                                              const int* __restrict__ rwin,
-                                                             const int* __restrict__ sc) {
+                                                             const int* __restrict__ sc, ChunkTiles T) {
+  if (T.och && (int)blockIdx.x == (int)gridDim.x - 1) {   // the extra workgroup: the pass's tile table
+    chunk_tiles_fwd(T, desc, st, sc, 2, ra == 0 ? sc + 1 : nullptr);
+    return;
+  }
   const RenderChunk ch = chunks[blockIdx.x];
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
@@ -787,7 +956,11 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_refine_emit(const
                                                              float4* __restrict__ cand, int* __restrict__ slotmap,
                                                              const uint64_t* __restrict__ rbits_g,
                                                              const uint64_t* __restrict__ abits_g,
-                                                             const int* __restrict__ ccnt) {
+                                                             const int* __restrict__ ccnt, ChunkTiles T) {
+  if (T.och && (int)blockIdx.x == (int)gridDim.x - 1) {   // the extra workgroup: the exact pass's tiles
+    chunk_tiles_fwd(T, desc, st, ccnt, 1, nullptr);
+    return;
+  }
   const RenderChunk ch = chunks[blockIdx.x];
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
@@ -825,115 +998,6 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_refine_emit(const
     S.n_emit = t;
     S.n_refine = t;
   }
-}
-
-// ------------------------------------------------------------------------------------
-// tile tables (single workgroup)
-// ------------------------------------------------------------------------------------
-// Tile tables (one block of 1024 threads): a block-wide exclusive scan of the per-object tile
-// counts gives every object its first tile; then the whole block writes the tiles, thread t
-// taking tiles t, t + 1024, ... of the chunk and finding its object by a binary search over
-// the chunk's first-tile offsets in LDS (one thread per object writing all of that object's
-// tiles was a serial loop of ~250 stores for one KITTI object's render pass, ~10 us).
-// Object order, then tile order within an object — the table the serial loop would build.
-constexpr int TILE_SCAN_THREADS = 1024;
-template <class Count, class Emit>
-__device__ __forceinline__ int tile_scan(int n_obj, int base, Count count, Emit emit) {
-  __shared__ int wsum[16];
-  __shared__ int carry;
-  __shared__ int first_s[TILE_SCAN_THREADS + 1];   // chunk-relative first tile per object, + total
-  __shared__ int n_s[TILE_SCAN_THREADS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-  if (tid == 0) carry = base;
-  __syncthreads();
-  for (int o0 = 0; o0 < n_obj; o0 += blockDim.x) {
-    const int o = o0 + tid;
-    const int m = min((int)blockDim.x, n_obj - o0);   // objects in this chunk
-    int n = 0, nt = 0;
-    if (o < n_obj) count(o, n, nt);
-    const int inc = wave_incl_scan(nt, lane);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    if (wv == 0) {
-      int v = lane < nw ? wsum[lane] : 0;
-      v = wave_incl_scan(v, lane);
-      if (lane < nw) wsum[lane] = v;
-    }
-    __syncthreads();
-    if (tid < m) {
-      first_s[tid] = (wv ? wsum[wv - 1] : 0) + inc - nt;
-      n_s[tid] = n;
-    }
-    if (tid == 0) first_s[m] = wsum[nw - 1];
-    __syncthreads();
-    const int c0 = carry, ct = first_s[m];
-    for (int t = tid; t < ct; t += blockDim.x) {
-      int lo = 0, hi = m - 1;                 // last object whose first tile is <= t
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (first_s[mid] <= t) lo = mid; else hi = mid - 1;
-      }
-      emit(c0 + t, o0 + lo, t - first_s[lo], n_s[lo]);
-    }
-    __syncthreads();
-    if (tid == 0) carry += ct;
-    __syncthreads();
-  }
-  return carry;
-}
-
-// with_pts (exact pass, kept masks): each object's sample tiles, then its surface-point
-// tiles (term 3, the same 64-point groups as the Jacobian's sdf tiles)
-__global__ void k_tiles_fwd(int n_obj, const ObjDesc* __restrict__ desc, const ObjState* __restrict__ st,
-                            Tile* __restrict__ tiles, int* __restrict__ n_tiles, int tsize, int with_pts) {
-  const int total = tile_scan(
-      n_obj, 0,
-      [&](int o, int& n, int& nt) {
-        const bool run = st[o].status == ST_RUNNING;
-        n = run ? st[o].n_emit : 0;
-        nt = (n + tsize - 1) / tsize;
-        if (with_pts && run) nt += (desc[o].n_pts + TILE - 1) / TILE;
-      },
-      [&](int idx, int o, int i, int n) {
-        Tile t;
-        const int nb = (n + tsize - 1) / tsize;
-        t.obj = o;
-        if (i < nb) {
-          t.term = 0; t.start = i * tsize;
-          t.count = min(tsize, n - i * tsize);
-        } else {
-          t.term = 3; t.start = (i - nb) * TILE;
-          t.count = min(TILE, desc[o].n_pts - t.start);
-        }
-        tiles[idx] = t;
-      });
-  if (threadIdx.x == 0) *n_tiles = total;
-}
-
-__global__ void k_tiles_jac(int n_obj, const ObjDesc* __restrict__ desc, ObjState* st,
-                            Tile* __restrict__ tiles, int* __restrict__ n_tiles) {
-  // Every object's sdf tiles (forward + backward) first, then every render tile (backward
-  // only, kept masks): the persistent grid's blocks then run tiles of one kind together, so
-  // the layers they stream stay in step (L2-resident weights).  Tile outputs go to slots
-  // derived from the tile itself (jac_tail), so the order changes no result.
-  int total = 0;
-  for (int term = 0; term < 2; ++term)
-    total = tile_scan(
-        n_obj, total,
-        [&](int o, int& n, int& nt) {
-          ObjState& S = st[o];
-          n = (S.status == ST_RUNNING) ? (term == 0 ? desc[o].n_pts : S.k) : 0;
-          nt = (n + TILE - 1) / TILE;
-          if (term == 0) S.n_sdf_tiles = nt;
-          else S.n_ren_tiles = nt;
-        },
-        [&](int idx, int o, int i, int n) {
-          Tile t;
-          t.obj = o; t.term = term; t.start = i * TILE;
-          t.count = min(TILE, n - i * TILE);
-          tiles[idx] = t;
-        });
-  if (threadIdx.x == 0) *n_tiles = total;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1181,7 +1245,14 @@ __global__ __launch_bounds__(256) void k_render_gather(const RenderChunk* __rest
                                                        const float4* __restrict__ kst,
                                                        const float* __restrict__ rst,
                                                        const int* __restrict__ sst, float4* __restrict__ kpts,
-                                                       float* __restrict__ kres, int* __restrict__ kslot) {
+                                                       float* __restrict__ kres, int* __restrict__ kslot,
+                                                       ChunkTiles T) {
+  if (T.och && (int)blockIdx.x == (int)gridDim.x - 1) {   // the extra workgroup: the Jacobian's tiles
+    build_tiles_jac(
+        T.n_obj, desc, st, [&](int o) { return object_chunk_sum(ccnt, 1, T.och[o].x, T.och[o].y); }, T.tiles,
+        T.n_tiles);
+    return;
+  }
   const RenderChunk ch = chunks[blockIdx.x];
   ObjState& S = st[ch.obj];
   if (S.status != ST_RUNNING) return;
