@@ -1127,6 +1127,15 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < M) dep_s[tid] = S.depths[tid];
   const int nr = min(RENDER_RAYS, d.n_rays - ch.ray0);
+  // this thread's ray: observed depth and direction, loaded now so their latency hides behind the
+  // staging below (used after the scans)
+  const int ray = ch.ray0 + tid;
+  float dob = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
+  if (tid < nr) {
+    dob = dobs_all[d.ray_off + ray];
+    const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
+    rx = rp[0]; ry = rp[1]; rz = rp[2];
+  }
   {
     // The chunk's rows are one contiguous run of nr * M floats: read as 16-byte loads (a scalar
     // head up to the first aligned address, a scalar tail), all of a thread's loads in flight
@@ -1167,11 +1176,10 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
   }
   __syncthreads();
   const float dmax = S.dmax, delta_d = S.delta_d;
-  const int ray = ch.ray0 + tid;
   float* Tr = T_s + tid * pitch;
   float* Dr = D_s + tid * pitch;                  // sdf row; a kept sample's slot then holds its de_do
   int cnt = 0, jend = 0;
-  float du = 0.f, dob = 0.f;
+  float du = 0.f;
   uint64_t keep = 0;
   if (tid < nr) {
     // cumprod of (1 - o) (loss.py:111, sequential in fp32 like torch's), term
@@ -1185,25 +1193,43 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
     float T = 1.f;
     double dud = 0.0;
     int j = 0;
+    float s_next = Tr[0], d_next = dep_s[0];       // (next sample's LDS reads issued a step early)
     for (; j < M && T != 0.f; ++j) {
-      const float s = Tr[j];
+      const float s = s_next, dj = d_next;
+      if (j + 1 < M) { s_next = Tr[j + 1]; d_next = dep_s[j + 1]; }
       const float ov = occupancy(s, nth, th, two_th);
       if (s > nth && s < th) grad |= 1ull << j;     // loss.py:101
       const float tp = ov * T;
       T = T * (1.f - ov);
       Tr[j] = T;
-      dud += (double)(dep_s[j] * tp);
+      dud += (double)(dj * tp);
     }
-    jend = j;                                       // Tr[l] = 0 for l >= jend
+    jend = j;                                       // (samples l >= jend: transmittance 0)
     dud += (double)((1.1f * dmax) * T);            // background bin o=1, d=1.1*d_max
     du = (float)dud;
-    dob = dobs_all[d.ray_off + ray];
-    for (uint64_t m = grad; m; m &= m - 1) {
-      const int jj = __builtin_ctzll(m);
-      double sacc = 0.0;
-      for (int l = jj; l < jend; ++l) sacc += (double)Tr[l];
-      const float dedo = (float)sacc / (1.f - occupancy(Dr[jj], nth, th, two_th));   // :131-132
-      if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; Dr[jj] = dedo; }              // :135
+    // de_do of each band sample jj: the transmittance tail sum over l = jj .. jend-1 in fp64 (:131),
+    // up to 4 band samples per sweep of the row, each sum still taken term by term from l = jj
+    for (uint64_t m = grad; m;) {
+      int jq[4];
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        jq[q] = m ? __builtin_ctzll(m) : jend;
+        m &= m - 1;
+      }
+      for (int l = jq[0]; l < jend; ++l) {
+        const double t = (double)Tr[l];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (l >= jq[q]) acc[q] += t;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int jj = jq[q];
+        if (jj >= jend) continue;
+        const float dedo = (float)acc[q] / (1.f - occupancy(Dr[jj], nth, th, two_th));   // :131-132
+        if (dedo > 1e-2f) { keep |= 1ull << jj; ++cnt; Dr[jj] = dedo; }                // :135
+      }
     }
   }
   const int inc = wave_incl_scan(cnt, lane);
@@ -1215,8 +1241,6 @@ __global__ __launch_bounds__(RENDER_RAYS) void k_render_rays(const RenderChunk* 
     float res = dob - du;                           // :145
     res = res > 0.30f ? 0.30f : res;                // :147-148
     res = res < -0.30f ? -0.30f : res;
-    const float* rp = rays_all + (size_t)(d.ray_off + ray) * 3;
-    const float rx = rp[0], ry = rp[1], rz = rp[2];
     const size_t base = (size_t)d.cand_off + (size_t)ch.ray0 * M;
     for (uint64_t m = keep; m; m &= m - 1) {
       const int jj = __builtin_ctzll(m);
