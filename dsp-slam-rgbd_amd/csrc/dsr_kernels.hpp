@@ -750,8 +750,10 @@ __global__ __launch_bounds__(RENDER_RAYS) DSR_NO_PK_F32 void k_sample_emit(const
 
 // ------------------------------------------------------------------------------------
 // k_sample_pass: the same pass in one 1024-thread workgroup per object walking its rays in
-// rounds (DSR_PRESCAN=0: the schedule tests' second implementation of the pass), first pass
-// included: it clears the dead flags, records the runs and counts n_valid itself.
+// rounds — the multi-group batches' form (measured equal to the chunked one there, DESIGN.md
+// §3.8) and, under DSR_PRESCAN=0, the schedule tests' second implementation for one group; the
+// first pass included: it clears the dead flags, records the runs and counts n_valid itself.
+// k_tiles_fwd then builds the pass's tile table from S.n_emit.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(SAMPLE_THREADS) DSR_NO_PK_F32 void k_sample_pass(int n_obj, const ObjDesc* __restrict__ desc,
                                                                 ObjState* st, const float* __restrict__ rays_all,
