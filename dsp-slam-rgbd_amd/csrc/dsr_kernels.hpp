@@ -1,7 +1,7 @@
 // dsr_kernels.hpp — the device-resident Gauss-Newton iteration of
 // Optimizer.reconstruct_object (reconstruct/optimizer.py:90-205) for a batch of
-// independent objects.  One iteration = 8 + 4 x (render passes) launches, none of which
-// needs the host:
+// independent objects.  One iteration = 9 + 3 x (render passes) launches per object group on
+// the chunked path (one group), 12 + 3 x (render passes) otherwise, none of which needs the host:
 //
 //   k_iter_begin   optimizer.py:122-128  t_cam_obj, scale, linspace depths, bg depth,
 //                                        + code folded into lin0 / lin4 biases
@@ -9,7 +9,8 @@
 //   k_sample_scan / k_sample_count + k_sample_emit
 //                  loss.py:71-88         ray samples -> object frame -> |x|<1 ->
 //                                        (ray, depth)-ordered compaction of live rays
-//   k_tiles_fwd    —                     64-point tiles over the pass's samples
+//   k_tiles_fwd    —                     tiles over the pass's samples (chunked path: built
+//                                        by an extra workgroup of k_sample_emit / k_refine_emit)
 //   k_mlp_fwd      loss.py:91-92         decode_sdf (MFMA), flags terminated rays
 //   k_render       loss.py:97-150        occupancy, transmittance cumprod, rendered
 //                                        depth, de_do, K-compaction, residual clamp
